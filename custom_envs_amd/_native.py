@@ -1,0 +1,106 @@
+"""ctypes binding of the HIP engine (include/custom_envs_amd.h).
+
+The product path has no CPU fallback: if the in-tree library is missing or
+cannot be loaded, importing the engine raises ``NativeEngineError``.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd.so')
+
+ABI_VERSION = 1
+CE_OK, CE_EINVAL, CE_EHIP, CE_ENOMEM, CE_ESTATE, CE_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
+CE_PROBLEM_SOFTMAX = 0
+CE_F64, CE_F32 = 0, 1
+CE_PTR_DEVICE = 1
+
+STATUS_NAMES = {CE_EINVAL: 'CE_EINVAL', CE_EHIP: 'CE_EHIP', CE_ENOMEM: 'CE_ENOMEM',
+                CE_ESTATE: 'CE_ESTATE', CE_EUNSUPPORTED: 'CE_EUNSUPPORTED'}
+
+# Every symbol include/custom_envs_amd.h declares.
+EXPORTS = (
+    'ce_abi_version', 'ce_last_error', 'ce_create', 'ce_destroy', 'ce_set_stream',
+    'ce_num_envs', 'ce_obs_dim', 'ce_act_dim', 'ce_seed', 'ce_seed_draws', 'ce_reset',
+    'ce_step', 'ce_step_async', 'ce_wait', 'ce_step_many', 'ce_host_outputs',
+    'ce_get_state', 'ce_set_state',
+)
+
+
+class NativeEngineError(RuntimeError):
+    """Raised when the HIP engine is missing or a C-ABI call fails."""
+
+
+class CeConfig(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_int32) for name in (
+        'abi_version', 'problem', 'precision', 'device', 'num_envs', 'n_rows',
+        'n_features', 'n_classes', 'batch_size', 'max_steps', 'auto_reset')]
+
+
+class CeOutputs(ctypes.Structure):
+    _fields_ = [('obs', ctypes.c_void_p), ('reward', ctypes.c_void_p),
+                ('done', ctypes.c_void_p), ('objective', ctypes.c_void_p),
+                ('accuracy', ctypes.c_void_p), ('episode_len', ctypes.c_void_p)]
+
+
+class CeState(ctypes.Structure):
+    _fields_ = [('weights', ctypes.c_void_p), ('grad_hist', ctypes.c_void_p),
+                ('loss_hist', ctypes.c_void_p), ('step', ctypes.c_void_p),
+                ('init_weights', ctypes.c_void_p), ('order', ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def _declare(lib):
+    vp, i32, u32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64
+    sig = {
+        'ce_abi_version': ([], ctypes.c_int),
+        'ce_last_error': ([], ctypes.c_char_p),
+        'ce_create': ([ctypes.POINTER(CeConfig), vp, vp, ctypes.POINTER(vp)], ctypes.c_int),
+        'ce_destroy': ([vp], None),
+        'ce_set_stream': ([vp, vp], ctypes.c_int),
+        'ce_num_envs': ([vp], ctypes.c_int),
+        'ce_obs_dim': ([vp], ctypes.c_int),
+        'ce_act_dim': ([vp], ctypes.c_int),
+        'ce_seed': ([vp, vp, i32], ctypes.c_int),
+        'ce_seed_draws': ([ctypes.c_uint64, i32, i32, i32, vp, vp], ctypes.c_int),
+        'ce_reset': ([vp, ctypes.POINTER(CeOutputs), u32], ctypes.c_int),
+        'ce_step': ([vp, vp, ctypes.POINTER(CeOutputs), u32], ctypes.c_int),
+        'ce_step_async': ([vp, vp, ctypes.POINTER(CeOutputs), u32], ctypes.c_int),
+        'ce_wait': ([vp], ctypes.c_int),
+        'ce_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeOutputs)], ctypes.c_int),
+        'ce_host_outputs': ([vp, ctypes.POINTER(CeOutputs)], ctypes.c_int),
+        'ce_get_state': ([vp, ctypes.POINTER(CeState)], ctypes.c_int),
+        'ce_set_state': ([vp, ctypes.POINTER(CeState)], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+def load():
+    """Load the in-tree engine library (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeEngineError(
+                'HIP engine library not built: %s (run python -m custom_envs_amd.build)'
+                % LIB_PATH)
+        try:
+            lib = ctypes.CDLL(LIB_PATH)
+        except OSError as err:
+            raise NativeEngineError('cannot load %s: %s' % (LIB_PATH, err)) from err
+        _declare(lib)
+        if lib.ce_abi_version() != ABI_VERSION:
+            raise NativeEngineError('engine ABI mismatch')
+        _lib = lib
+    return _lib
+
+
+def check(rc, what):
+    if rc != CE_OK:
+        msg = load().ce_last_error().decode(errors='replace')
+        raise NativeEngineError('%s: %s (%s)' % (what, msg, STATUS_NAMES.get(rc, rc)))
+    return rc

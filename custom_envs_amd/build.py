@@ -1,0 +1,77 @@
+"""Build the in-tree HIP engine library for gfx950.
+
+    python -m custom_envs_amd.build            # -> custom_envs_amd/lib/*.so
+
+hipcc compiles the kernels for gfx950 only (no host fallback, no other
+arch); seeding.cpp is plain host C++.  The library has no torch dependency:
+Python binds it with ctypes (custom_envs_amd/_native.py).
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, 'csrc')
+LIBDIR = os.path.join(HERE, 'lib')
+LIBNAME = 'libcustom_envs_amd.so'
+ARCH = 'gfx950'
+
+
+def _hipcc():
+    for cand in (os.environ.get('HIPCC'), '/opt/rocm/bin/hipcc', shutil.which('hipcc')):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError('hipcc not found; the engine requires ROCm (gfx950)')
+
+
+def sources():
+    return [os.path.join(CSRC, f) for f in ('engine.hip', 'seeding.cpp')]
+
+
+def headers():
+    return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'seeding.h')] + [
+        os.path.join(ROOT, 'include', 'custom_envs_amd.h')]
+
+
+def lib_path():
+    return os.path.join(LIBDIR, LIBNAME)
+
+
+def up_to_date():
+    out = lib_path()
+    if not os.path.exists(out):
+        return False
+    mtime = os.path.getmtime(out)
+    return all(os.path.getmtime(p) <= mtime for p in sources() + headers())
+
+
+def build(force=False, verbose=False):
+    if not force and up_to_date():
+        return lib_path()
+    os.makedirs(LIBDIR, exist_ok=True)
+    hipcc = _hipcc()
+    objs = []
+    common = ['-O3', '-fPIC', '-std=c++17', '-Wall', '-I', os.path.join(ROOT, 'include')]
+    tmp = os.path.join(LIBDIR, 'obj')
+    os.makedirs(tmp, exist_ok=True)
+    for src in sources():
+        obj = os.path.join(tmp, os.path.basename(src) + '.o')
+        if src.endswith('.hip'):
+            cmd = [hipcc, '--offload-arch=' + ARCH, '-x', 'hip'] + common + ['-c', src, '-o', obj]
+        else:
+            cmd = [hipcc, '-x', 'c++'] + common + ['-c', src, '-o', obj]
+        if verbose:
+            print(' '.join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    out = lib_path()
+    cmd = [hipcc, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out + '.tmp'] + objs
+    subprocess.run(cmd, check=True)
+    os.replace(out + '.tmp', out)
+    return out
+
+
+if __name__ == '__main__':
+    print(build(force='--force' in sys.argv, verbose=True))

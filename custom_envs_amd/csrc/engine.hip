@@ -1,0 +1,512 @@
+// C-ABI implementation of the MI355X Optimize-v0 engine (include/custom_envs_amd.h).
+//
+// Host responsibilities: own the device copy of the dataset and the per-env
+// state (struct-of-arrays, one contiguous [E][P] slab per quantity so a
+// wave's P values are one coalesced segment), stage host actions/outputs
+// through pinned buffers, and launch one fused step kernel per VecEnv.step
+// (optimize_kernels.h).  The env RNG is native (seeding.cpp): W0 and the
+// reset permutation are drawn once per seed and uploaded, because
+// use_random_state never advances the env RNG (custom_envs/utils/
+// utils_math.py:9-22), so every reset replays the same draws.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/custom_envs_amd.h"
+#include "optimize_kernels.h"
+#include "seeding.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define CE_HIP(call)                                                            \
+    do {                                                                        \
+        hipError_t err_ = (call);                                               \
+        if (err_ != hipSuccess)                                                 \
+            return fail(CE_EHIP, std::string(#call " failed: ") +               \
+                                     hipGetErrorString(err_));                  \
+    } while (0)
+
+using StepFn = void (*)(const void *args, int grid, hipStream_t stream);
+
+template <typename T, int F, int K>
+void launch_step(const void *args, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL((ce::optimize_step_kernel<T, F, K>), dim3(grid), dim3(ce::kBlock), 0,
+                       stream, *static_cast<const ce::StepArgs<T> *>(args));
+}
+
+template <typename T, int F, int K>
+void launch_reset(const void *args, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL((ce::optimize_reset_kernel<T, F, K>), dim3(grid), dim3(ce::kBlock), 0,
+                       stream, *static_cast<const ce::StepArgs<T> *>(args));
+}
+
+struct KernelEntry {
+    int precision, F, K;
+    StepFn step, reset;
+};
+
+// Shapes with a compiled register-path instance (F*K + 2 <= 64).
+#define CE_SHAPES(X) \
+    X(2, 2) X(4, 2) X(4, 3) X(5, 2) X(8, 2) X(10, 2) X(16, 2) X(20, 2) X(10, 3) X(10, 4) X(3, 3)
+
+#define CE_ENTRY(F, K)                                                           \
+    {CE_F64, F, K, launch_step<double, F, K>, launch_reset<double, F, K>},       \
+    {CE_F32, F, K, launch_step<float, F, K>, launch_reset<float, F, K>},
+
+const KernelEntry kKernels[] = {CE_SHAPES(CE_ENTRY)};
+
+const KernelEntry *find_kernel(int precision, int F, int K) {
+    for (const auto &k : kKernels)
+        if (k.precision == precision && k.F == F && k.K == K) return &k;
+    return nullptr;
+}
+
+size_t align16(size_t v) { return (v + 15) & ~static_cast<size_t>(15); }
+
+}  // namespace
+
+struct ce_engine {
+    ce_config cfg{};
+    int P = 0, obs_dim = 0;
+    size_t tsize = 8;  // sizeof(T)
+    const KernelEntry *kern = nullptr;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    // device state
+    void *X = nullptr;
+    int32_t *label = nullptr;
+    void *W = nullptr, *G = nullptr, *W0 = nullptr;
+    double *L = nullptr;
+    int32_t *step = nullptr;
+    int32_t *perm = nullptr, *order = nullptr, *order_sel = nullptr;
+    float *d_act = nullptr;
+    // outputs: one region on the device, a pinned mirror on the host
+    size_t off[6] = {0};
+    size_t out_bytes = 0;
+    char *d_out = nullptr;
+    char *h_out = nullptr;
+    float *h_act = nullptr;
+    bool was_reset = false;
+    // ce_step_many graph cache
+    hipGraphExec_t graph = nullptr;
+    int graph_k = 0;
+    const float *graph_act = nullptr;
+    int64_t graph_stride = 0;
+    ce_outputs graph_out{};
+    hipStream_t graph_stream = nullptr;
+};
+
+namespace {
+
+ce_outputs region_view(const ce_engine *e, char *base) {
+    ce_outputs o;
+    o.obs = reinterpret_cast<float *>(base + e->off[0]);
+    o.reward = reinterpret_cast<float *>(base + e->off[1]);
+    o.objective = reinterpret_cast<float *>(base + e->off[2]);
+    o.accuracy = reinterpret_cast<float *>(base + e->off[3]);
+    o.episode_len = reinterpret_cast<int32_t *>(base + e->off[4]);
+    o.done = reinterpret_cast<uint8_t *>(base + e->off[5]);
+    return o;
+}
+
+template <typename T>
+ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs &o) {
+    ce::StepArgs<T> a;
+    a.E = e->cfg.num_envs;
+    a.N = e->cfg.n_rows;
+    a.B = e->cfg.batch_size;
+    a.max_steps = e->cfg.max_steps;
+    a.auto_reset = e->cfg.auto_reset;
+    a.X = static_cast<const T *>(e->X);
+    a.label = e->label;
+    a.W = static_cast<T *>(e->W);
+    a.G = static_cast<T *>(e->G);
+    a.L = e->L;
+    a.step = e->step;
+    a.W0 = static_cast<const T *>(e->W0);
+    a.perm = e->perm;
+    a.order = e->order;
+    a.order_sel = e->order_sel;
+    a.act = act;
+    a.obs = o.obs;
+    a.reward = o.reward;
+    a.done = o.done;
+    a.objective = o.objective;
+    a.accuracy = o.accuracy;
+    a.episode_len = o.episode_len;
+    return a;
+}
+
+int grid_of(const ce_engine *e) {
+    return (e->cfg.num_envs + ce::kWavesPerBlock - 1) / ce::kWavesPerBlock;
+}
+
+void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &o,
+            hipStream_t stream) {
+    StepFn fn = reset ? e->kern->reset : e->kern->step;
+    if (e->cfg.precision == CE_F64) {
+        auto a = make_args<double>(e, act, o);
+        fn(&a, grid_of(e), stream);
+    } else {
+        auto a = make_args<float>(e, act, o);
+        fn(&a, grid_of(e), stream);
+    }
+}
+
+// Convert host float64 rows to the engine's compute type and upload.
+int upload_typed(ce_engine *e, void *dst, const double *src, size_t count) {
+    if (e->cfg.precision == CE_F64) {
+        CE_HIP(hipMemcpyAsync(dst, src, count * sizeof(double), hipMemcpyHostToDevice, e->stream));
+    } else {
+        std::vector<float> tmp(count);
+        for (size_t i = 0; i < count; ++i) tmp[i] = static_cast<float>(src[i]);
+        CE_HIP(hipMemcpyAsync(dst, tmp.data(), count * sizeof(float), hipMemcpyHostToDevice,
+                              e->stream));
+        CE_HIP(hipStreamSynchronize(e->stream));
+    }
+    return CE_OK;
+}
+
+int download_typed(ce_engine *e, double *dst, const void *src, size_t count) {
+    if (e->cfg.precision == CE_F64) {
+        CE_HIP(hipMemcpyAsync(dst, src, count * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+        CE_HIP(hipStreamSynchronize(e->stream));
+    } else {
+        std::vector<float> tmp(count);
+        CE_HIP(hipMemcpyAsync(tmp.data(), src, count * sizeof(float), hipMemcpyDeviceToHost,
+                              e->stream));
+        CE_HIP(hipStreamSynchronize(e->stream));
+        for (size_t i = 0; i < count; ++i) dst[i] = tmp[i];
+    }
+    return CE_OK;
+}
+
+void copy_out(const ce_engine *e, const ce_outputs &src, const ce_outputs *dst) {
+    const size_t E = e->cfg.num_envs;
+    if (!dst) return;
+    if (dst->obs) std::memcpy(dst->obs, src.obs, E * e->obs_dim * sizeof(float));
+    if (dst->reward) std::memcpy(dst->reward, src.reward, E * sizeof(float));
+    if (dst->done) std::memcpy(dst->done, src.done, E);
+    if (dst->objective) std::memcpy(dst->objective, src.objective, E * sizeof(float));
+    if (dst->accuracy) std::memcpy(dst->accuracy, src.accuracy, E * sizeof(float));
+    if (dst->episode_len) std::memcpy(dst->episode_len, src.episode_len, E * sizeof(int32_t));
+}
+
+bool complete(const ce_outputs *o) {
+    return o && o->obs && o->reward && o->done && o->objective && o->accuracy && o->episode_len;
+}
+
+int do_step(ce_engine *e, const float *actions, const ce_outputs *out, uint32_t flags,
+            bool sync) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    if (!e->was_reset) return fail(CE_ESTATE, "step() before the first reset()");
+    if (!actions) return fail(CE_EINVAL, "null actions");
+    const size_t E = e->cfg.num_envs;
+    if (flags & CE_PTR_DEVICE) {
+        ce_outputs o = out ? *out : region_view(e, e->d_out);
+        if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+        launch(e, false, actions, o, e->stream);
+        CE_HIP(hipGetLastError());
+        if (sync) CE_HIP(hipStreamSynchronize(e->stream));
+        return CE_OK;
+    }
+    std::memcpy(e->h_act, actions, E * e->P * sizeof(float));
+    CE_HIP(hipMemcpyAsync(e->d_act, e->h_act, E * e->P * sizeof(float), hipMemcpyHostToDevice,
+                          e->stream));
+    launch(e, false, e->d_act, region_view(e, e->d_out), e->stream);
+    CE_HIP(hipGetLastError());
+    CE_HIP(hipMemcpyAsync(e->h_out, e->d_out, e->out_bytes, hipMemcpyDeviceToHost, e->stream));
+    if (sync) {
+        CE_HIP(hipStreamSynchronize(e->stream));
+        copy_out(e, region_view(e, e->h_out), out);
+    }
+    return CE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ce_abi_version(void) { return CE_ABI_VERSION; }
+
+const char *ce_last_error(void) { return g_last_error.c_str(); }
+
+int ce_seed_draws(uint64_t seed, int32_t n_features, int32_t n_classes, int32_t n_rows,
+                  double *init_weights, int32_t *perm) {
+    if (n_features <= 0 || n_classes <= 0 || n_rows < 0)
+        return fail(CE_EINVAL, "ce_seed_draws: bad shape");
+    ce::reset_draws(seed, n_features, n_classes, n_rows, init_weights, perm);
+    return CE_OK;
+}
+
+int ce_create(const ce_config *cfg, const double *features, const int32_t *labels,
+              ce_engine **out) {
+    if (!cfg || !features || !labels || !out) return fail(CE_EINVAL, "ce_create: null argument");
+    *out = nullptr;
+    if (cfg->abi_version != CE_ABI_VERSION)
+        return fail(CE_EINVAL, "ce_create: ABI version mismatch");
+    if (cfg->problem != CE_PROBLEM_SOFTMAX)
+        return fail(CE_EUNSUPPORTED, "ce_create: unknown problem");
+    if (cfg->precision != CE_F64 && cfg->precision != CE_F32)
+        return fail(CE_EINVAL, "ce_create: unknown precision");
+    if (cfg->num_envs <= 0 || cfg->n_rows <= 0 || cfg->n_features <= 0 || cfg->n_classes <= 0)
+        return fail(CE_EINVAL, "ce_create: sizes must be positive");
+    if (cfg->batch_size <= 0 || cfg->batch_size > cfg->n_rows)
+        return fail(CE_EINVAL, "ce_create: batch_size must be in [1, n_rows]");
+    if (cfg->max_steps <= 0) return fail(CE_EINVAL, "ce_create: max_steps must be positive");
+    const KernelEntry *kern = find_kernel(cfg->precision, cfg->n_features, cfg->n_classes);
+    if (!kern)
+        return fail(CE_EUNSUPPORTED, "ce_create: no compiled kernel for F=" +
+                                         std::to_string(cfg->n_features) +
+                                         " K=" + std::to_string(cfg->n_classes));
+    for (int i = 0; i < cfg->n_rows; ++i)
+        if (labels[i] < 0 || labels[i] >= cfg->n_classes)
+            return fail(CE_EINVAL, "ce_create: label out of range");
+
+    ce_engine *e = new (std::nothrow) ce_engine();
+    if (!e) return fail(CE_ENOMEM, "ce_create: host allocation failed");
+    e->cfg = *cfg;
+    e->kern = kern;
+    e->P = cfg->n_features * cfg->n_classes;
+    e->obs_dim = 2 * e->P + 1;
+    e->tsize = cfg->precision == CE_F64 ? sizeof(double) : sizeof(float);
+    auto bail = [&](int code) {
+        ce_destroy(e);
+        return code;
+    };
+    int rc;
+#define CE_TRY(call)                                                   \
+    do {                                                               \
+        hipError_t err_ = (call);                                      \
+        if (err_ != hipSuccess)                                        \
+            return bail(fail(CE_EHIP, std::string(#call " failed: ") + \
+                                          hipGetErrorString(err_)));   \
+    } while (0)
+    CE_TRY(hipSetDevice(cfg->device));
+    CE_TRY(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+    e->stream = e->own_stream;
+
+    const size_t E = cfg->num_envs, N = cfg->n_rows, F = cfg->n_features, P = e->P;
+    CE_TRY(hipMalloc(&e->X, N * F * e->tsize));
+    CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
+    CE_TRY(hipMalloc(&e->W, E * P * e->tsize));
+    CE_TRY(hipMalloc(&e->G, E * P * e->tsize));
+    CE_TRY(hipMalloc(&e->W0, E * P * e->tsize));
+    CE_TRY(hipMalloc(&e->L, E * sizeof(double)));
+    CE_TRY(hipMalloc(&e->step, E * sizeof(int32_t)));
+    CE_TRY(hipMalloc(&e->d_act, E * P * sizeof(float)));
+    CE_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_act), E * P * sizeof(float)));
+    if (cfg->batch_size < cfg->n_rows) {
+        CE_TRY(hipMalloc(&e->perm, E * N * sizeof(int32_t)));
+        CE_TRY(hipMalloc(&e->order, 2 * E * N * sizeof(int32_t)));
+        CE_TRY(hipMalloc(&e->order_sel, E * sizeof(int32_t)));
+        std::vector<int32_t> ident(E * N);
+        for (size_t i = 0; i < E; ++i)
+            for (size_t r = 0; r < N; ++r) ident[i * N + r] = static_cast<int32_t>(r);
+        CE_TRY(hipMemcpy(e->order, ident.data(), E * N * sizeof(int32_t), hipMemcpyHostToDevice));
+        CE_TRY(hipMemcpy(e->perm, ident.data(), E * N * sizeof(int32_t), hipMemcpyHostToDevice));
+        CE_TRY(hipMemset(e->order_sel, 0, E * sizeof(int32_t)));
+    }
+    size_t off = 0;
+    const size_t sizes[6] = {E * e->obs_dim * sizeof(float), E * sizeof(float), E * sizeof(float),
+                             E * sizeof(float), E * sizeof(int32_t), E};
+    for (int i = 0; i < 6; ++i) {
+        e->off[i] = off;
+        off = align16(off + sizes[i]);
+    }
+    e->out_bytes = off;
+    CE_TRY(hipMalloc(&e->d_out, e->out_bytes));
+    CE_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_out), e->out_bytes));
+    CE_TRY(hipMemset(e->d_out, 0, e->out_bytes));
+    std::memset(e->h_out, 0, e->out_bytes);
+    CE_TRY(hipMemset(e->G, 0, E * P * e->tsize));
+    CE_TRY(hipMemset(e->L, 0, E * sizeof(double)));
+    CE_TRY(hipMemset(e->step, 0, E * sizeof(int32_t)));
+#undef CE_TRY
+    if ((rc = upload_typed(e, e->X, features, N * F)) != CE_OK) return bail(rc);
+    if (hipMemcpy(e->label, labels, N * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(CE_EHIP, "ce_create: label upload failed"));
+    // Unseeded envs behave like np_random(None): os.urandom seeds.  The host
+    // side normally seeds explicitly; default to seed = env index here.
+    std::vector<uint64_t> seeds(E);
+    for (size_t i = 0; i < E; ++i) seeds[i] = i;
+    if ((rc = ce_seed(e, seeds.data(), static_cast<int32_t>(E))) != CE_OK) return bail(rc);
+    if (hipStreamSynchronize(e->stream) != hipSuccess)
+        return bail(fail(CE_EHIP, "ce_create: sync failed"));
+    *out = e;
+    return CE_OK;
+}
+
+void ce_destroy(ce_engine *e) {
+    if (!e) return;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->graph) (void)hipGraphExecDestroy(e->graph);
+    void *dev[] = {e->X, e->label, e->W, e->G, e->W0, e->L, e->step,
+                   e->perm, e->order, e->order_sel, e->d_act, e->d_out};
+    for (void *p : dev)
+        if (p) (void)hipFree(p);
+    if (e->h_out) (void)hipHostFree(e->h_out);
+    if (e->h_act) (void)hipHostFree(e->h_act);
+    if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+    delete e;
+}
+
+int ce_set_stream(ce_engine *e, void *stream) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    e->stream = stream ? static_cast<hipStream_t>(stream) : e->own_stream;
+    return CE_OK;
+}
+
+int ce_num_envs(const ce_engine *e) { return e ? e->cfg.num_envs : CE_EINVAL; }
+int ce_obs_dim(const ce_engine *e) { return e ? e->obs_dim : CE_EINVAL; }
+int ce_act_dim(const ce_engine *e) { return e ? e->P : CE_EINVAL; }
+
+int ce_seed(ce_engine *e, const uint64_t *seeds, int32_t n) {
+    if (!e || !seeds) return fail(CE_EINVAL, "ce_seed: null argument");
+    if (n != e->cfg.num_envs) return fail(CE_EINVAL, "ce_seed: need one seed per env");
+    const size_t E = n, P = e->P, N = e->cfg.n_rows;
+    const bool with_perm = e->perm != nullptr;
+    std::vector<double> w0(E * P);
+    std::vector<int32_t> perm(with_perm ? E * N : 0);
+    for (size_t i = 0; i < E; ++i)
+        ce::reset_draws(seeds[i], e->cfg.n_features, e->cfg.n_classes, static_cast<int>(N),
+                        &w0[i * P], with_perm ? &perm[i * N] : nullptr);
+    int rc = upload_typed(e, e->W0, w0.data(), E * P);
+    if (rc != CE_OK) return rc;
+    if (with_perm)
+        CE_HIP(hipMemcpyAsync(e->perm, perm.data(), E * N * sizeof(int32_t),
+                              hipMemcpyHostToDevice, e->stream));
+    CE_HIP(hipStreamSynchronize(e->stream));
+    return CE_OK;
+}
+
+int ce_reset(ce_engine *e, const ce_outputs *out, uint32_t flags) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    if (flags & CE_PTR_DEVICE) {
+        if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+        ce_outputs o = out ? *out : region_view(e, e->d_out);
+        launch(e, true, nullptr, o, e->stream);
+        CE_HIP(hipGetLastError());
+        e->was_reset = true;
+        return CE_OK;
+    }
+    launch(e, true, nullptr, region_view(e, e->d_out), e->stream);
+    CE_HIP(hipGetLastError());
+    CE_HIP(hipMemcpyAsync(e->h_out, e->d_out, e->out_bytes, hipMemcpyDeviceToHost, e->stream));
+    CE_HIP(hipStreamSynchronize(e->stream));
+    e->was_reset = true;
+    if (out && out->obs)
+        std::memcpy(out->obs, region_view(e, e->h_out).obs,
+                    static_cast<size_t>(e->cfg.num_envs) * e->obs_dim * sizeof(float));
+    return CE_OK;
+}
+
+int ce_step(ce_engine *e, const float *actions, const ce_outputs *out, uint32_t flags) {
+    return do_step(e, actions, out, flags, true);
+}
+
+int ce_step_async(ce_engine *e, const float *actions, const ce_outputs *out, uint32_t flags) {
+    return do_step(e, actions, out, flags, false);
+}
+
+int ce_wait(ce_engine *e) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    CE_HIP(hipStreamSynchronize(e->stream));
+    return CE_OK;
+}
+
+int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
+                 const ce_outputs *out) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
+    if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "ce_step_many: bad arguments");
+    if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+    const ce_outputs o = out ? *out : region_view(e, e->d_out);
+    const bool hit = e->graph && e->graph_k == k && e->graph_act == actions &&
+                     e->graph_stride == stride && e->graph_stream == e->stream &&
+                     std::memcmp(&e->graph_out, &o, sizeof(o)) == 0;
+    if (!hit) {
+        if (e->graph) {
+            CE_HIP(hipGraphExecDestroy(e->graph));
+            e->graph = nullptr;
+        }
+        hipGraph_t g;
+        CE_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+        for (int s = 0; s < k; ++s) launch(e, false, actions + s * stride, o, e->stream);
+        CE_HIP(hipStreamEndCapture(e->stream, &g));
+        hipError_t err = hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (err != hipSuccess)
+            return fail(CE_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(err));
+        e->graph_k = k;
+        e->graph_act = actions;
+        e->graph_stride = stride;
+        e->graph_out = o;
+        e->graph_stream = e->stream;
+    }
+    CE_HIP(hipGraphLaunch(e->graph, e->stream));
+    return CE_OK;
+}
+
+int ce_host_outputs(ce_engine *e, ce_outputs *view) {
+    if (!e || !view) return fail(CE_EINVAL, "null argument");
+    *view = region_view(e, e->h_out);
+    return CE_OK;
+}
+
+int ce_get_state(ce_engine *e, const ce_state *st) {
+    if (!e || !st) return fail(CE_EINVAL, "null argument");
+    const size_t E = e->cfg.num_envs, P = e->P, N = e->cfg.n_rows;
+    int rc;
+    CE_HIP(hipStreamSynchronize(e->stream));
+    if (st->weights && (rc = download_typed(e, st->weights, e->W, E * P)) != CE_OK) return rc;
+    if (st->grad_hist && (rc = download_typed(e, st->grad_hist, e->G, E * P)) != CE_OK) return rc;
+    if (st->init_weights && (rc = download_typed(e, st->init_weights, e->W0, E * P)) != CE_OK)
+        return rc;
+    if (st->loss_hist) CE_HIP(hipMemcpy(st->loss_hist, e->L, E * sizeof(double), hipMemcpyDeviceToHost));
+    if (st->step) CE_HIP(hipMemcpy(st->step, e->step, E * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (st->order) {
+        if (!e->order) return fail(CE_ESTATE, "row order is only tracked when batch_size < n_rows");
+        std::vector<int32_t> sel(E), both(2 * E * N);
+        CE_HIP(hipMemcpy(sel.data(), e->order_sel, E * sizeof(int32_t), hipMemcpyDeviceToHost));
+        CE_HIP(hipMemcpy(both.data(), e->order, 2 * E * N * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < E; ++i)
+            std::memcpy(st->order + i * N, &both[sel[i] * E * N + i * N], N * sizeof(int32_t));
+    }
+    return CE_OK;
+}
+
+int ce_set_state(ce_engine *e, const ce_state *st) {
+    if (!e || !st) return fail(CE_EINVAL, "null argument");
+    const size_t E = e->cfg.num_envs, P = e->P, N = e->cfg.n_rows;
+    int rc;
+    CE_HIP(hipStreamSynchronize(e->stream));
+    if (st->weights && (rc = upload_typed(e, e->W, st->weights, E * P)) != CE_OK) return rc;
+    if (st->grad_hist && (rc = upload_typed(e, e->G, st->grad_hist, E * P)) != CE_OK) return rc;
+    if (st->init_weights && (rc = upload_typed(e, e->W0, st->init_weights, E * P)) != CE_OK)
+        return rc;
+    if (st->loss_hist) CE_HIP(hipMemcpy(e->L, st->loss_hist, E * sizeof(double), hipMemcpyHostToDevice));
+    if (st->step) CE_HIP(hipMemcpy(e->step, st->step, E * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (st->order) {
+        if (!e->order) return fail(CE_ESTATE, "row order is only tracked when batch_size < n_rows");
+        CE_HIP(hipMemcpy(e->order, st->order, E * N * sizeof(int32_t), hipMemcpyHostToDevice));
+        CE_HIP(hipMemset(e->order_sel, 0, E * sizeof(int32_t)));
+    }
+    CE_HIP(hipStreamSynchronize(e->stream));
+    e->was_reset = true;
+    return CE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,32 @@
+// Native restatement of gym<=0.21 np_random + numpy RandomState draws.
+#pragma once
+#include <cstdint>
+
+namespace ce {
+
+struct Mt19937 {
+    static constexpr int kN = 624, kM = 397;
+    uint32_t mt[kN];
+    int pos = kN;
+    bool has_gauss = false;
+    double gauss = 0.0;
+
+    void init_by_array(const uint32_t *key, int n);
+    void generate();
+    uint32_t next32();
+    double next_double();
+    double next_gauss();
+    uint64_t interval(uint64_t max);
+};
+
+// Key words RandomState.seed() receives for gym's np_random(seed); returns
+// the key length (1 or 2).
+int seed_key(uint64_t seed, uint32_t key[2]);
+
+// (W0, perm) drawn by every reset of an env seeded with `seed`: F*K legacy
+// gaussians in C order, then a legacy shuffle of arange(n_rows).  Either
+// output may be null.
+void reset_draws(uint64_t seed, int n_features, int n_classes, int n_rows,
+                 double *init_weights, int32_t *perm);
+
+}  // namespace ce

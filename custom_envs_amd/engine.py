@@ -1,0 +1,210 @@
+"""Python handle on one HIP Optimize-v0 engine (one GPU, E envs).
+
+``OptimizeEngine`` is the thin host layer over the C ABI: it builds the
+config, seeds envs with gym semantics, and moves actions/outputs either
+through the engine's pinned host buffers (numpy in, numpy out) or straight
+between device tensors (``step_device``; torch tensors on the engine
+stream, no host round trip).  There is no CPU fallback: constructing an
+engine without the HIP library or without a GPU raises
+``NativeEngineError``.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from custom_envs_amd import _native
+from custom_envs_amd._native import CeConfig, CeOutputs, CeState, check
+
+PRECISIONS = {'f64': _native.CE_F64, 'float64': _native.CE_F64,
+              'f32': _native.CE_F32, 'float32': _native.CE_F32}
+
+
+def normalize_seed(seed):
+    """gym ``create_seed``: None -> 64 random bits, int -> int mod 2**64."""
+    if seed is None:
+        return int.from_bytes(os.urandom(8), 'little')
+    if isinstance(seed, (int, np.integer)) and seed >= 0:
+        return int(seed) % (1 << 64)
+    raise ValueError('seed must be a non-negative integer or None, got %r' % (seed,))
+
+
+def labels_from_targets(targets):
+    """Class index per row of one-hot targets (argmax(Y), optimize.py:94-96)."""
+    targets = np.asarray(targets)
+    if targets.ndim == 1:
+        return targets.astype(np.int32), int(targets.max()) + 1
+    return np.argmax(targets, axis=1).astype(np.int32), targets.shape[1]
+
+
+def _view(ptr, count, ctype, dtype, shape):
+    buf = (ctype * count).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype).reshape(shape)
+
+
+class OptimizeEngine:
+    """E Optimize-v0 environments advanced in lock step on one GPU."""
+
+    def __init__(self, features, targets, num_envs, batch_size=None, max_steps=40,
+                 precision='f64', device=0, auto_reset=True):
+        lib = _native.load()
+        features = np.ascontiguousarray(features, dtype=np.float64)
+        labels, n_classes = labels_from_targets(targets)
+        n_rows, n_features = features.shape
+        if len(labels) != n_rows:
+            raise ValueError('features and targets differ in length')
+        self.num_envs = int(num_envs)
+        self.n_rows, self.n_features, self.n_classes = n_rows, n_features, n_classes
+        self.batch_size = n_rows if batch_size is None else int(batch_size)
+        self.max_steps = int(max_steps)
+        self.precision = precision
+        self.device = int(device)
+        cfg = CeConfig(abi_version=_native.ABI_VERSION, problem=_native.CE_PROBLEM_SOFTMAX,
+                       precision=PRECISIONS[precision], device=self.device,
+                       num_envs=self.num_envs, n_rows=n_rows, n_features=n_features,
+                       n_classes=n_classes, batch_size=self.batch_size,
+                       max_steps=self.max_steps, auto_reset=1 if auto_reset else 0)
+        self._labels = np.ascontiguousarray(labels, dtype=np.int32)
+        handle = ctypes.c_void_p()
+        check(lib.ce_create(ctypes.byref(cfg), features.ctypes.data, self._labels.ctypes.data,
+                            ctypes.byref(handle)), 'ce_create')
+        self._lib = lib
+        self._h = handle
+        self.act_dim = lib.ce_act_dim(handle)
+        self.obs_dim = lib.ce_obs_dim(handle)
+        view = CeOutputs()
+        check(lib.ce_host_outputs(handle, ctypes.byref(view)), 'ce_host_outputs')
+        E = self.num_envs
+        self._host = {
+            'obs': _view(view.obs, E * self.obs_dim, ctypes.c_float, np.float32,
+                         (E, self.obs_dim)),
+            'reward': _view(view.reward, E, ctypes.c_float, np.float32, (E,)),
+            'done': _view(view.done, E, ctypes.c_uint8, np.uint8, (E,)),
+            'objective': _view(view.objective, E, ctypes.c_float, np.float32, (E,)),
+            'accuracy': _view(view.accuracy, E, ctypes.c_float, np.float32, (E,)),
+            'episode_len': _view(view.episode_len, E, ctypes.c_int32, np.int32, (E,)),
+        }
+        self.seeds = [None] * E
+
+    # ------------------------------------------------------------------ seeding
+    def seed(self, seeds):
+        """Seed every env (``BaseEnvironment.seed``, baseenvironment.py:20-28)."""
+        if seeds is None or isinstance(seeds, (int, np.integer)):
+            seeds = [seeds] * self.num_envs if seeds is None else [
+                int(seeds) + i for i in range(self.num_envs)]
+        seeds = [normalize_seed(s) for s in seeds]
+        if len(seeds) != self.num_envs:
+            raise ValueError('need one seed per env')
+        arr = np.array(seeds, dtype=np.uint64)
+        check(self._lib.ce_seed(self._h, arr.ctypes.data, self.num_envs), 'ce_seed')
+        self.seeds = seeds
+        return seeds
+
+    # --------------------------------------------------------------- host mode
+    def reset(self):
+        check(self._lib.ce_reset(self._h, None, 0), 'ce_reset')
+        return self._host['obs'].copy()
+
+    def step_async(self, actions):
+        actions = np.ascontiguousarray(actions, dtype=np.float32)
+        if actions.shape != (self.num_envs, self.act_dim):
+            actions = actions.reshape(self.num_envs, self.act_dim)
+        self._pending = actions   # keep alive until the H2D copy is done
+        check(self._lib.ce_step_async(self._h, actions.ctypes.data, None, 0), 'ce_step_async')
+
+    def step_wait(self):
+        """Return views of the pinned outputs (valid until the next step)."""
+        check(self._lib.ce_wait(self._h), 'ce_wait')
+        self._pending = None
+        return self._host
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    # ------------------------------------------------------------- device mode
+    def set_stream(self, stream_handle):
+        check(self._lib.ce_set_stream(self._h, ctypes.c_void_p(stream_handle or 0)),
+              'ce_set_stream')
+
+    @staticmethod
+    def _outputs(out):
+        return CeOutputs(obs=out['obs'].data_ptr(), reward=out['reward'].data_ptr(),
+                         done=out['done'].data_ptr(), objective=out['objective'].data_ptr(),
+                         accuracy=out['accuracy'].data_ptr(),
+                         episode_len=out['episode_len'].data_ptr())
+
+    def alloc_device_outputs(self, torch_device=None):
+        import torch
+        dev = torch_device or torch.device('cuda', self.device)
+        E = self.num_envs
+        return {'obs': torch.empty((E, self.obs_dim), dtype=torch.float32, device=dev),
+                'reward': torch.empty(E, dtype=torch.float32, device=dev),
+                'done': torch.empty(E, dtype=torch.uint8, device=dev),
+                'objective': torch.empty(E, dtype=torch.float32, device=dev),
+                'accuracy': torch.empty(E, dtype=torch.float32, device=dev),
+                'episode_len': torch.empty(E, dtype=torch.int32, device=dev)}
+
+    def _check_device_tensors(self, actions, out, steps=1):
+        if actions.dtype.itemsize != 4 or not actions.is_contiguous():
+            raise ValueError('actions must be a contiguous float32 device tensor')
+        if actions.numel() < steps * self.num_envs * self.act_dim:
+            raise ValueError('actions tensor too small')
+        for key, t in out.items():
+            if not t.is_contiguous():
+                raise ValueError('output %s must be contiguous' % key)
+        if out['obs'].numel() != self.num_envs * self.obs_dim:
+            raise ValueError('obs output has the wrong size')
+
+    def reset_device(self, out):
+        o = self._outputs(out)
+        check(self._lib.ce_reset(self._h, ctypes.byref(o), _native.CE_PTR_DEVICE),
+              'ce_reset')
+
+    def step_device(self, actions, out):
+        """Stream-ordered step from a device action tensor into device outputs."""
+        self._check_device_tensors(actions, out)
+        o = self._outputs(out)
+        check(self._lib.ce_step_async(self._h, actions.data_ptr(), ctypes.byref(o),
+                                      _native.CE_PTR_DEVICE), 'ce_step_async')
+
+    def step_many_device(self, k, actions, out, per_step_actions=True):
+        """k stream-ordered steps (one hipGraph); actions [k][E][P] or [E][P]."""
+        self._check_device_tensors(actions, out, k if per_step_actions else 1)
+        stride = self.num_envs * self.act_dim if per_step_actions else 0
+        o = self._outputs(out)
+        check(self._lib.ce_step_many(self._h, int(k), actions.data_ptr(), stride,
+                                     ctypes.byref(o)), 'ce_step_many')
+
+    def wait(self):
+        check(self._lib.ce_wait(self._h), 'ce_wait')
+
+    # ------------------------------------------------------------------ state
+    def get_state(self):
+        E, P, N = self.num_envs, self.act_dim, self.n_rows
+        st = {'weights': np.zeros((E, P)), 'grad_hist': np.zeros((E, P)),
+              'loss_hist': np.zeros(E), 'step': np.zeros(E, np.int32),
+              'init_weights': np.zeros((E, P))}
+        if self.batch_size < N:
+            st['order'] = np.zeros((E, N), np.int32)
+        cst = CeState(**{k: v.ctypes.data for k, v in st.items()})
+        check(self._lib.ce_get_state(self._h, ctypes.byref(cst)), 'ce_get_state')
+        return st
+
+    def set_state(self, **state):
+        conv = {'weights': np.float64, 'grad_hist': np.float64, 'loss_hist': np.float64,
+                'step': np.int32, 'init_weights': np.float64, 'order': np.int32}
+        arrays = {k: np.ascontiguousarray(v, dtype=conv[k]) for k, v in state.items()}
+        cst = CeState(**{k: v.ctypes.data for k, v in arrays.items()})
+        check(self._lib.ce_set_state(self._h, ctypes.byref(cst)), 'ce_set_state')
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._lib.ce_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

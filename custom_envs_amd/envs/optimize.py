@@ -1,0 +1,69 @@
+"""Optimize-v0 as a single gym env: a one-env view of the HIP engine.
+
+Reference: custom_envs/envs/optimize.py:14-109 over
+custom_envs/envs/baseenvironment.py:11-57.  Same constructor keywords
+(``data_set``, ``batch_size``, ``n_of_steps``), same spaces, same old-gym
+4-tuple step and info keys.  The dynamics run in the fused HIP kernel with
+``auto_reset`` off, so stepping past the terminal step behaves like the
+reference (current_step keeps counting, ``done`` stays True).
+"""
+import numpy as np
+
+from custom_envs_amd.core import Env
+from custom_envs_amd.data import load_data
+from custom_envs_amd.dataset import InMemoryDataSet
+from custom_envs_amd.spaces import Box
+
+
+def resolve_dataset(data_set, batch_size):
+    """Accept a load_data name, an InMemoryDataSet or a (features, targets) pair."""
+    if isinstance(data_set, InMemoryDataSet):
+        features, targets = data_set.features, data_set.targets
+    elif isinstance(data_set, (tuple, list)):
+        features, targets = data_set
+    else:
+        seq = load_data(data_set, batch_size)
+        features, targets = seq.features, seq.targets
+    return np.asarray(features, dtype=np.float64), np.asarray(targets)
+
+
+def optimize_spaces(n_params):
+    """optimize.py:51-55."""
+    obs = Box(low=-1e3, high=1e3, dtype=np.float32, shape=(2 * n_params + 1,))
+    act = Box(low=-1e3, high=1e3, dtype=np.float32, shape=(n_params,))
+    return obs, act
+
+
+class Optimize(Env):
+    """Agent subtracts its action from a softmax classifier's weights."""
+    metadata = {'render.modes': []}
+
+    def __init__(self, data_set='gaussians_256x10', batch_size=None, n_of_steps=None,
+                 max_steps=40, precision='f64', device=0):
+        from custom_envs_amd.engine import OptimizeEngine
+        features, targets = resolve_dataset(data_set, batch_size)
+        self.engine = OptimizeEngine(features, targets, 1, batch_size=batch_size,
+                                     max_steps=max_steps, precision=precision,
+                                     device=device, auto_reset=False)
+        self.current_step = 0
+        self.observation_space, self.action_space = optimize_spaces(self.engine.act_dim)
+        self.seed()
+
+    def seed(self, seed=None):
+        return self.engine.seed([seed])
+
+    def reset(self):
+        self.current_step = 0
+        return self.engine.reset()[0]
+
+    def step(self, action):
+        out = self.engine.step(np.asarray(action, dtype=np.float32).reshape(1, -1))
+        self.current_step = int(out['episode_len'][0])
+        reward = float(out['reward'][0])
+        info = {'objective': float(out['objective'][0]),
+                'accuracy': float(out['accuracy'][0]),
+                'episode': {'r': reward, 'l': self.current_step}}
+        return out['obs'][0].copy(), reward, bool(out['done'][0]), info
+
+    def close(self):
+        self.engine.close()

@@ -1,0 +1,5 @@
+"""Vectorised environments (replaces custom_envs/vectorize/__init__.py:1-3)."""
+from custom_envs_amd.vectorize.concurrent import SubprocVecEnv, ThreadVecEnv
+from custom_envs_amd.vectorize.gpuvecenv import GPUVecEnv, LazyInfos
+
+__all__ = ['GPUVecEnv', 'LazyInfos', 'SubprocVecEnv', 'ThreadVecEnv']

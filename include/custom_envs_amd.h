@@ -1,0 +1,150 @@
+/*
+ * custom_envs_amd -- C ABI of the MI355X vectorised Optimize-v0 engine.
+ *
+ * The reference (adolfogonzalez3/custom_envs) is pure Python and has no FFI;
+ * every entry point below replaces one Python-level interface on the hot
+ * path, cited as file:line relative to the reference root:
+ *
+ *   ce_create      Optimize.__init__            custom_envs/envs/optimize.py:40-56
+ *                  + ConcurrentVecEnv.__init__   custom_envs/vectorize/concurrentvecenv.py:77-95
+ *   ce_seed        BaseEnvironment.seed          custom_envs/envs/baseenvironment.py:20-28
+ *   ce_seed_draws  Optimize.base_reset draws     custom_envs/envs/optimize.py:63-64
+ *                  (model.reset then sequence.shuffle under use_random_state,
+ *                   custom_envs/utils/utils_math.py:9-22)
+ *   ce_reset       ConcurrentVecEnv.reset        custom_envs/vectorize/concurrentvecenv.py:109-113
+ *                  -> BaseEnvironment.reset       custom_envs/envs/baseenvironment.py:43-49
+ *   ce_step        VecEnv.step = step_async+step_wait
+ *                                                custom_envs/vectorize/concurrentvecenv.py:97-107
+ *                  -> _worker 'step' + auto-reset custom_envs/utils/utils_venv.py:24-56 (:31)
+ *                  -> BaseEnvironment.step        custom_envs/envs/baseenvironment.py:30-41
+ *                  -> Optimize.base_step          custom_envs/envs/optimize.py:69-100
+ *   ce_step_async  ConcurrentVecEnv.step_async   custom_envs/vectorize/concurrentvecenv.py:97-100
+ *   ce_wait        ConcurrentVecEnv.step_wait    custom_envs/vectorize/concurrentvecenv.py:102-107
+ *   ce_step_many   K consecutive VecEnv.step calls with device-resident actions
+ *                  (benchmark / GPU-resident agent mode; one hipGraph)
+ *   ce_get_state / ce_set_state
+ *                  the per-env attributes model.weights, loss_hist, grad_hist,
+ *                  current_step (optimize.py:45-50, baseenvironment.py:18)
+ *   ce_destroy     ConcurrentVecEnv.close        custom_envs/vectorize/concurrentvecenv.py:115-125
+ *
+ * Conventions
+ *   - Every function returns CE_OK (0) or a negative ce_status; nothing
+ *     throws across the ABI.  ce_last_error() returns a thread-local message.
+ *   - The engine owns all device memory (dataset, per-env state).  The caller
+ *     owns the buffers it passes in.  With CE_PTR_DEVICE the caller's
+ *     pointers are device pointers and the call is stream-ordered
+ *     (asynchronous) on the engine stream (ce_set_stream); otherwise they are
+ *     host pointers and the call synchronises before returning.
+ *   - One engine per host thread; calls on one engine are not re-entrant.
+ */
+#ifndef CUSTOM_ENVS_AMD_H
+#define CUSTOM_ENVS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CE_ABI_VERSION 1
+
+typedef struct ce_engine ce_engine;
+
+typedef enum ce_status {
+    CE_OK = 0,
+    CE_EINVAL = -1,      /* bad argument or configuration                 */
+    CE_EHIP = -2,        /* HIP runtime error                             */
+    CE_ENOMEM = -3,      /* allocation failed                             */
+    CE_ESTATE = -4,      /* e.g. step before the first reset              */
+    CE_EUNSUPPORTED = -5 /* shape has no compiled kernel instance         */
+} ce_status;
+
+typedef enum ce_problem {
+    /* softmax classifier without bias (the missing ModelNumpy) */
+    CE_PROBLEM_SOFTMAX = 0
+} ce_problem;
+
+typedef enum ce_precision {
+    CE_F64 = 0, /* float64 state and arithmetic (the reference's numpy dtype) */
+    CE_F32 = 1  /* float32 arithmetic, float64 loss recurrence                 */
+} ce_precision;
+
+enum {
+    CE_PTR_DEVICE = 1u << 0 /* pointers passed to the call are device pointers */
+};
+
+typedef struct ce_config {
+    int32_t abi_version; /* CE_ABI_VERSION                                  */
+    int32_t problem;     /* ce_problem                                      */
+    int32_t precision;   /* ce_precision                                    */
+    int32_t device;      /* HIP device ordinal                              */
+    int32_t num_envs;    /* E: envs owned by this engine (one rank's shard) */
+    int32_t n_rows;      /* N: dataset rows                                 */
+    int32_t n_features;  /* F                                               */
+    int32_t n_classes;   /* K (targets are one-hot, to_onehot semantics)    */
+    int32_t batch_size;  /* B rows per minibatch; B == N for batch_size=None */
+    int32_t max_steps;   /* episode length, optimize.py:102-103 (40)        */
+    int32_t auto_reset;  /* 1: VecEnv auto-reset on done (utils_venv.py:31);
+                            0: single gym.Env (baseenvironment.py:30-41)   */
+} ce_config;
+
+/* Per-step outputs, one row per env.  obs is [E][2P+1] with P = F*K. */
+typedef struct ce_outputs {
+    float *obs;        /* concat(wght_hist[idx], loss_hist[idx], grad_hist[idx]) */
+    float *reward;     /* -loss (minibatch, after the update)                */
+    uint8_t *done;     /* current_step >= max_steps                          */
+    float *objective;  /* info['objective']: full-dataset loss               */
+    float *accuracy;   /* info['accuracy']                                   */
+    int32_t *episode_len; /* info['episode']['l'] (current_step of the step) */
+} ce_outputs;
+
+/* Host-side copies of the per-env state (any pointer may be NULL). */
+typedef struct ce_state {
+    double *weights;      /* [E][P]  model.weights                         */
+    double *grad_hist;    /* [E][P]  grad_hist[idx] of the last step       */
+    double *loss_hist;    /* [E]     loss_hist[idx] of the last step       */
+    int32_t *step;        /* [E]     current_step                          */
+    double *init_weights; /* [E][P]  W0 every reset restores               */
+    int32_t *order;       /* [E][N]  current row order (B < N only)        */
+} ce_state;
+
+int ce_abi_version(void);
+const char *ce_last_error(void);
+
+int ce_create(const ce_config *cfg, const double *features /* [N][F] */,
+              const int32_t *labels /* [N] class index */, ce_engine **out);
+void ce_destroy(ce_engine *eng);
+
+int ce_set_stream(ce_engine *eng, void *hip_stream /* NULL: engine's own */);
+int ce_num_envs(const ce_engine *eng);
+int ce_obs_dim(const ce_engine *eng);
+int ce_act_dim(const ce_engine *eng);
+
+/* seeds[i] seeds env i exactly as gym.utils.seeding.np_random(seeds[i]). */
+int ce_seed(ce_engine *eng, const uint64_t *seeds, int32_t n);
+/* Host-only: the (W0, perm) that every reset of a seed draws.  No GPU. */
+int ce_seed_draws(uint64_t seed, int32_t n_features, int32_t n_classes,
+                  int32_t n_rows, double *init_weights, int32_t *perm);
+
+int ce_reset(ce_engine *eng, const ce_outputs *out, uint32_t flags);
+int ce_step(ce_engine *eng, const float *actions /* [E][P] */,
+            const ce_outputs *out, uint32_t flags);
+int ce_step_async(ce_engine *eng, const float *actions, const ce_outputs *out,
+                  uint32_t flags);
+int ce_wait(ce_engine *eng);
+int ce_step_many(ce_engine *eng, int32_t k, const float *actions,
+                 int64_t action_step_stride /* elements between steps */,
+                 const ce_outputs *out /* device pointers */);
+
+/* Pinned host buffers holding the last host-mode outputs (zero-copy views). */
+int ce_host_outputs(ce_engine *eng, ce_outputs *view);
+
+int ce_get_state(ce_engine *eng, const ce_state *st);
+int ce_set_state(ce_engine *eng, const ce_state *st);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CUSTOM_ENVS_AMD_H */

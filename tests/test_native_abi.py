@@ -1,0 +1,100 @@
+"""The C-ABI library: builds, loads, exports every declared symbol, seeds.
+
+No compute call here needs a GPU: ce_seed_draws is host-only, and ce_create
+on a GPU-less machine must fail loudly (CE_EHIP) instead of falling back.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden
+from custom_envs_amd import _native
+
+
+def _declared_functions():
+    text = open(os.path.join(ROOT, 'include', 'custom_envs_amd.h')).read()
+    return set(re.findall(r'^\s*(?:const\s+)?\w+\s+\**\s*(ce_\w+)\s*\(', text, re.M))
+
+
+def test_library_loads():
+    lib = _native.load()
+    assert lib.ce_abi_version() == _native.ABI_VERSION
+
+
+def test_every_declared_symbol_is_exported():
+    lib = _native.load()
+    declared = _declared_functions()
+    assert declared == set(_native.EXPORTS)
+    for name in declared:
+        assert hasattr(lib, name), name
+
+
+def test_config_struct_matches_header():
+    text = open(os.path.join(ROOT, 'include', 'custom_envs_amd.h')).read()
+    body = text[text.index('typedef struct ce_config'):text.index('} ce_config;')]
+    fields = re.findall(r'int32_t\s+(\w+);', body)
+    assert fields == [f[0] for f in _native.CeConfig._fields_]
+
+
+def test_native_seeding_matches_numpy_and_hashlib():
+    lib = _native.load()
+    fx = golden('seeding.npz')
+    n_rows = fx['perms'].shape[1]
+    for i, seed in enumerate(fx['seeds']):
+        w0 = np.zeros((10, 2))
+        perm = np.zeros(n_rows, np.int32)
+        _native.check(lib.ce_seed_draws(int(seed), 10, 2, n_rows, w0.ctypes.data,
+                                        perm.ctypes.data), 'ce_seed_draws')
+        assert np.array_equal(w0, fx['weights'][i])
+        assert np.array_equal(perm, fx['perms'][i])
+    w0 = np.zeros((3, 3))
+    perm = np.zeros(150, np.int32)
+    _native.check(lib.ce_seed_draws(5, 3, 3, 150, w0.ctypes.data, perm.ctypes.data), 'draw')
+    assert np.array_equal(w0, fx['w_odd']) and np.array_equal(perm, fx['p_odd'])
+
+
+@pytest.mark.parametrize('seed', [0, 3, 2**31 - 1, 2**33, 2**64 - 1])
+def test_native_seeding_against_live_numpy(seed):
+    from oracle.optimize import initial_draws
+    lib = _native.load()
+    w_ref, p_ref = initial_draws(seed, 4, 3, 97)
+    w0 = np.zeros((4, 3))
+    perm = np.zeros(97, np.int32)
+    _native.check(lib.ce_seed_draws(seed, 4, 3, 97, w0.ctypes.data, perm.ctypes.data), 'draw')
+    assert np.array_equal(w0, w_ref) and np.array_equal(perm, p_ref)
+
+
+def test_bad_arguments_are_reported():
+    lib = _native.load()
+    assert lib.ce_seed_draws(0, 0, 2, 4, None, None) == _native.CE_EINVAL
+    assert b'bad shape' in lib.ce_last_error()
+    handle = ctypes.c_void_p()
+    cfg = _native.CeConfig(abi_version=999)
+    x = np.zeros((4, 2))
+    y = np.zeros(4, np.int32)
+    assert lib.ce_create(ctypes.byref(cfg), x.ctypes.data, y.ctypes.data,
+                         ctypes.byref(handle)) == _native.CE_EINVAL
+    assert b'ABI' in lib.ce_last_error()
+
+
+def test_unsupported_shape_is_loud():
+    lib = _native.load()
+    cfg = _native.CeConfig(abi_version=_native.ABI_VERSION, num_envs=1, n_rows=4,
+                           n_features=7, n_classes=5, batch_size=4, max_steps=40)
+    x = np.zeros((4, 7))
+    y = np.zeros(4, np.int32)
+    handle = ctypes.c_void_p()
+    assert lib.ce_create(ctypes.byref(cfg), x.ctypes.data, y.ctypes.data,
+                         ctypes.byref(handle)) == _native.CE_EUNSUPPORTED
+
+
+def test_engine_without_gpu_fails_loudly(lr_dataset):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('a GPU is present')
+    from custom_envs_amd.engine import OptimizeEngine
+    with pytest.raises(_native.NativeEngineError):
+        OptimizeEngine(*lr_dataset, num_envs=2)
