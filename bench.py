@@ -262,6 +262,11 @@ def main():
                 'kernel_ms_mean': kernel_ms_mean,
                 'kernel': 'ce::optimize_step_kernel<%s,10,2>' % (
                     'double' if args.precision == 'f64' else 'float'),
+                # the limiter is the f64/f32 VALU, not HBM:
+                # algorithmic FLOPs 2NFK (logits) + 2NFK (X^T(P-Y)) + 5NK
+                'flops_per_env_step': 4 * 256 * P + 5 * 256 * 2,
+                'valu_tflops': (4 * 256 * P + 5 * 256 * 2) * E / (kernel_ms * 1e-3) / 1e12,
+                'valu_peak_tflops': F64_VALU_PEAK_TFLOPS if args.precision == 'f64' else 157.3,
             },
             'cpu_baseline': cpu,
             'host_loop_env_steps_per_s': host_rate,

@@ -16,6 +16,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 LIBDIR = os.path.join(HERE, 'lib')
 LIBNAME = 'libcustom_envs_amd.so'
+DIAG_LIBNAME = 'libcustom_envs_amd_diag.so'   # -DCE_DIAG phase stamps (profiling only)
 ARCH = 'gfx950'
 
 
@@ -35,26 +36,28 @@ def headers():
         os.path.join(ROOT, 'include', 'custom_envs_amd.h')]
 
 
-def lib_path():
-    return os.path.join(LIBDIR, LIBNAME)
+def lib_path(diag=False):
+    return os.path.join(LIBDIR, DIAG_LIBNAME if diag else LIBNAME)
 
 
-def up_to_date():
-    out = lib_path()
+def up_to_date(diag=False):
+    out = lib_path(diag)
     if not os.path.exists(out):
         return False
     mtime = os.path.getmtime(out)
     return all(os.path.getmtime(p) <= mtime for p in sources() + headers())
 
 
-def build(force=False, verbose=False):
-    if not force and up_to_date():
-        return lib_path()
+def build(force=False, verbose=False, diag=False):
+    if not force and up_to_date(diag):
+        return lib_path(diag)
     os.makedirs(LIBDIR, exist_ok=True)
     hipcc = _hipcc()
     objs = []
     common = ['-O3', '-fPIC', '-std=c++17', '-Wall', '-I', os.path.join(ROOT, 'include')]
-    tmp = os.path.join(LIBDIR, 'obj')
+    if diag:
+        common.append('-DCE_DIAG')
+    tmp = os.path.join(LIBDIR, 'obj_diag' if diag else 'obj')
     os.makedirs(tmp, exist_ok=True)
     for src in sources():
         obj = os.path.join(tmp, os.path.basename(src) + '.o')
@@ -66,7 +69,7 @@ def build(force=False, verbose=False):
             print(' '.join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    out = lib_path()
+    out = lib_path(diag)
     cmd = [hipcc, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out + '.tmp'] + objs
     subprocess.run(cmd, check=True)
     os.replace(out + '.tmp', out)
@@ -75,3 +78,5 @@ def build(force=False, verbose=False):
 
 if __name__ == '__main__':
     print(build(force='--force' in sys.argv, verbose=True))
+    if '--diag' in sys.argv:
+        print(build(force='--force' in sys.argv, verbose=True, diag=True))

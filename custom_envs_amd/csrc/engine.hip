@@ -38,32 +38,35 @@ int fail(int code, const std::string &msg) {
                                      hipGetErrorString(err_));                  \
     } while (0)
 
-using StepFn = void (*)(const void *args, int grid, hipStream_t stream);
+using StepFn = void (*)(const void *args, int grid, size_t lds, hipStream_t stream);
 
-template <typename T, int F, int K>
-void launch_step(const void *args, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL((ce::optimize_step_kernel<T, F, K>), dim3(grid), dim3(ce::kBlock), 0,
-                       stream, *static_cast<const ce::StepArgs<T> *>(args));
+template <typename T, int F, int K, bool STAGED>
+void launch_step(const void *args, int grid, size_t lds, hipStream_t stream) {
+    hipLaunchKernelGGL((ce::optimize_step_kernel<T, F, K, STAGED>), dim3(grid),
+                       dim3(ce::kBlock), STAGED ? lds : 0, stream,
+                       *static_cast<const ce::StepArgs<T> *>(args));
 }
 
 template <typename T, int F, int K>
-void launch_reset(const void *args, int grid, hipStream_t stream) {
+void launch_reset(const void *args, int grid, size_t, hipStream_t stream) {
     hipLaunchKernelGGL((ce::optimize_reset_kernel<T, F, K>), dim3(grid), dim3(ce::kBlock), 0,
                        stream, *static_cast<const ce::StepArgs<T> *>(args));
 }
 
 struct KernelEntry {
     int precision, F, K;
-    StepFn step, reset;
+    StepFn step_staged, step_global, reset;
 };
 
-// Shapes with a compiled register-path instance (F*K + 2 <= 64).
+// Shapes with a compiled register-path instance.
 #define CE_SHAPES(X) \
     X(2, 2) X(4, 2) X(4, 3) X(5, 2) X(8, 2) X(10, 2) X(16, 2) X(20, 2) X(10, 3) X(10, 4) X(3, 3)
 
-#define CE_ENTRY(F, K)                                                           \
-    {CE_F64, F, K, launch_step<double, F, K>, launch_reset<double, F, K>},       \
-    {CE_F32, F, K, launch_step<float, F, K>, launch_reset<float, F, K>},
+#define CE_ENTRY(F, K)                                                                \
+    {CE_F64, F, K, launch_step<double, F, K, true>, launch_step<double, F, K, false>, \
+     launch_reset<double, F, K>},                                                     \
+    {CE_F32, F, K, launch_step<float, F, K, true>, launch_step<float, F, K, false>,   \
+     launch_reset<float, F, K>},
 
 const KernelEntry kKernels[] = {CE_SHAPES(CE_ENTRY)};
 
@@ -99,6 +102,8 @@ struct ce_engine {
     char *h_out = nullptr;
     float *h_act = nullptr;
     bool was_reset = false;
+    bool staged = false;      // dataset fits the per-block LDS stage
+    size_t stage_bytes = 0;
     // ce_step_many graph cache
     hipGraphExec_t graph = nullptr;
     int graph_k = 0;
@@ -106,6 +111,7 @@ struct ce_engine {
     int64_t graph_stride = 0;
     ce_outputs graph_out{};
     hipStream_t graph_stream = nullptr;
+    unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
 };
 
 namespace {
@@ -129,8 +135,7 @@ ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs
     a.B = e->cfg.batch_size;
     a.max_steps = e->cfg.max_steps;
     a.auto_reset = e->cfg.auto_reset;
-    a.X = static_cast<const T *>(e->X);
-    a.label = e->label;
+    a.data = static_cast<const unsigned char *>(e->X);
     a.W = static_cast<T *>(e->W);
     a.G = static_cast<T *>(e->G);
     a.L = e->L;
@@ -146,6 +151,7 @@ ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs
     a.objective = o.objective;
     a.accuracy = o.accuracy;
     a.episode_len = o.episode_len;
+    a.diag = e->diag;
     return a;
 }
 
@@ -155,13 +161,13 @@ int grid_of(const ce_engine *e) {
 
 void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &o,
             hipStream_t stream) {
-    StepFn fn = reset ? e->kern->reset : e->kern->step;
+    StepFn fn = reset ? e->kern->reset : (e->staged ? e->kern->step_staged : e->kern->step_global);
     if (e->cfg.precision == CE_F64) {
         auto a = make_args<double>(e, act, o);
-        fn(&a, grid_of(e), stream);
+        fn(&a, grid_of(e), e->stage_bytes, stream);
     } else {
         auto a = make_args<float>(e, act, o);
-        fn(&a, grid_of(e), stream);
+        fn(&a, grid_of(e), e->stage_bytes, stream);
     }
 }
 
@@ -299,8 +305,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     e->stream = e->own_stream;
 
     const size_t E = cfg->num_envs, N = cfg->n_rows, F = cfg->n_features, P = e->P;
-    CE_TRY(hipMalloc(&e->X, N * F * e->tsize));
-    CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
+    CE_TRY(hipMalloc(&e->X, ce::stage_bytes_total(cfg->n_features, cfg->n_rows, static_cast<int>(e->tsize))));
     CE_TRY(hipMalloc(&e->W, E * P * e->tsize));
     CE_TRY(hipMalloc(&e->G, E * P * e->tsize));
     CE_TRY(hipMalloc(&e->W0, E * P * e->tsize));
@@ -328,6 +333,9 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     }
     e->out_bytes = off;
     CE_TRY(hipMalloc(&e->d_out, e->out_bytes));
+#ifdef CE_DIAG
+    CE_TRY(hipMalloc(&e->diag, E * ce::kStamps * sizeof(unsigned long long)));
+#endif
     CE_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_out), e->out_bytes));
     CE_TRY(hipMemset(e->d_out, 0, e->out_bytes));
     std::memset(e->h_out, 0, e->out_bytes);
@@ -335,9 +343,26 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     CE_TRY(hipMemset(e->L, 0, E * sizeof(double)));
     CE_TRY(hipMemset(e->step, 0, E * sizeof(int32_t)));
 #undef CE_TRY
-    if ((rc = upload_typed(e, e->X, features, N * F)) != CE_OK) return bail(rc);
-    if (hipMemcpy(e->label, labels, N * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
-        return bail(fail(CE_EHIP, "ce_create: label upload failed"));
+    // [rows | labels]: row-major rows padded to ce::row_stride elements (zeros
+    // in the pad), then the int32 labels, in one buffer staged with one copy
+    const size_t RS = ce::row_stride(cfg->n_features, static_cast<int>(e->tsize));
+    const size_t xbytes = ce::align16(N * RS * e->tsize);
+    std::vector<unsigned char> blob(ce::align16(xbytes + 4 * N), 0);
+    for (size_t r = 0; r < N; ++r)
+        for (size_t f = 0; f < F; ++f) {
+            const double v = features[r * F + f];
+            if (cfg->precision == CE_F64) {
+                std::memcpy(&blob[(r * RS + f) * 8], &v, 8);
+            } else {
+                const float v32 = static_cast<float>(v);
+                std::memcpy(&blob[(r * RS + f) * 4], &v32, 4);
+            }
+        }
+    std::memcpy(&blob[xbytes], labels, 4 * N);
+    if (hipMemcpy(e->X, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(CE_EHIP, "ce_create: dataset upload failed"));
+    e->stage_bytes = ce::stage_bytes_total(cfg->n_features, cfg->n_rows, static_cast<int>(e->tsize));
+    e->staged = e->stage_bytes <= ce::kStageLimit;
     // Unseeded envs behave like np_random(None): os.urandom seeds.  The host
     // side normally seeds explicitly; default to seed = env index here.
     std::vector<uint64_t> seeds(E);
@@ -354,7 +379,7 @@ void ce_destroy(ce_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->graph) (void)hipGraphExecDestroy(e->graph);
     void *dev[] = {e->X, e->label, e->W, e->G, e->W0, e->L, e->step,
-                   e->perm, e->order, e->order_sel, e->d_act, e->d_out};
+                   e->perm, e->order, e->order_sel, e->d_act, e->d_out, e->diag};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
@@ -465,6 +490,17 @@ int ce_host_outputs(ce_engine *e, ce_outputs *view) {
     *view = region_view(e, e->h_out);
     return CE_OK;
 }
+
+#ifdef CE_DIAG
+// Diagnostic builds only (not part of include/custom_envs_amd.h).
+int ce_diag_stamps(ce_engine *e, unsigned long long *out) {
+    if (!e || !out) return fail(CE_EINVAL, "null argument");
+    CE_HIP(hipStreamSynchronize(e->stream));
+    CE_HIP(hipMemcpy(out, e->diag, sizeof(unsigned long long) * e->cfg.num_envs * ce::kStamps,
+                     hipMemcpyDeviceToHost));
+    return CE_OK;
+}
+#endif
 
 int ce_get_state(ce_engine *e, const ce_state *st) {
     if (!e || !st) return fail(CE_EINVAL, "null argument");

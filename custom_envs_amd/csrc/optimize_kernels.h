@@ -17,28 +17,64 @@
 //   reward = -loss, done = step >= max_steps, info = full-data (loss, acc)
 //   done -> W <- W0, G <- 0, L <- 0, step <- 0, order <- order[perm]
 //
-// Lane mapping: minibatch row i of an env lives on lane i % 64 (chunks of
-// 64 rows).  W is broadcast from lanes 0..P-1 into scalar registers with
-// v_readlane, so the row loop is VGPR(x) x SGPR(w) FMAs.  The P gradient
-// partials, the loss and the hit count are combined by a recursive-halving
-// reduce-scatter over the wave (log2(NP) xor-shuffle levels moving NP-1
-// values instead of NP*6), after which lane l owns element l >> S.
+// Layout and mapping
+//   - The dataset is stored row-major with rows padded to an odd number of
+//     16-byte units (row_stride) and staged once per workgroup into LDS (16
+//     envs share one copy): a row is F/2 conflict-free ds_read_b128 at
+//     immediate offsets.
+//   - Minibatch row i of an env lives on lane i % 64 (chunks of 64 rows).
+//   - W is broadcast from lanes 0..P-1 into scalar registers (v_readlane):
+//     the row loop is VGPR(x) x SGPR(w) FMAs.
+//   - K = 2 (the benchmark problem) uses the two-class form of the same
+//     softmax: z = x.(w0 - w1), t = exp(-|z|), p_max = 1/(1+t),
+//     p_min = t/(1+t): one exp, one reciprocal and one log per row, and
+//     column 1 of X^T(P-Y) is exactly minus column 0.
+//   - p_y - 1 is formed as -(sum of the other classes' p), which is the
+//     same number without the cancellation.
+//   - Gradient partials, the loss and the hit count are combined by a
+//     recursive-halving reduce-scatter over the wave (log2(NP) xor-shuffle
+//     levels moving NP-1 values instead of NP*6), after which lane l owns
+//     element l >> S.
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace ce {
 
 constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;
+constexpr int kWavesPerBlock = 16;
 constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr size_t kStageLimit = 64 * 1024;   // LDS bytes a block may stage
+
+// Near-minimax (Chebyshev-fitted) polynomials for the two-class fast path:
+//   exp(r),  |r| <= ln2/2 : degree 10, rel. err 6.7e-16 (c0 = 1 exactly, so
+//                           exp(0) == 1 as in libm)
+//   atanh(s)/s = g(s^2), s^2 <= 0.02944 : degree 6 in s^2, rel. err 4.4e-16
+// (fits: scripts/fit_poly.py).  Horner order is from the top coefficient.
+constexpr int kExpTerms = 11;
+constexpr int kLogTerms = 7;
+constexpr double kExpCoef[kExpTerms] = {
+    1.0, 1.000000000000006, 0.49999999999997946, 0.16666666666560392,
+    0.041666666667466275, 0.008333333384270189, 0.0013888888768614806,
+    0.00019841171680137992, 2.4801650828121558e-05, 2.7639677785365415e-06,
+    2.7575738554394086e-07};
+constexpr double kLogCoef[kLogTerms] = {
+    1.0, 0.33333333333278237, 0.20000000030151868, 0.14285708126945562,
+    0.11111708755950479, 0.09061251072084696, 0.08415323922275515};
+constexpr double kLn2Hi = 6.93147180369123816490e-01;
+constexpr double kLn2Lo = 1.90821492927058770002e-10;
+constexpr double kLog2e = 1.44269504088896338700e+00;
+
+template <typename T>
+struct MathConsts {};
 
 template <typename T>
 struct StepArgs {
     int E, N, B, max_steps, auto_reset;
-    const T *X;            // [N][F] row-major dataset (device copy, type T)
-    const int32_t *label;  // [N] class index (one-hot targets)
+    const unsigned char *data;  // [N][RS] rows (padded, row_stride) then [N] int32 labels
     T *W;                  // [E][P] model.weights
     T *G;                  // [E][P] grad_hist[idx] of the last step
     double *L;             // [E]    loss_hist[idx] of the last step
@@ -54,7 +90,65 @@ struct StepArgs {
     float *objective;
     float *accuracy;
     int32_t *episode_len;
+    unsigned long long *diag;   // [E][kStamps] (CE_DIAG builds only)
 };
+
+// Diagnostic builds (-DCE_DIAG) stamp s_memtime at phase boundaries into a
+// per-wave record; product builds compile the stamps away.
+#ifdef CE_DIAG
+#define CE_STAMP(k)                                                              \
+    do {                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                       \
+        unsigned long long t_;                                                   \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                       \
+        stamps[k] = t_;                                                          \
+    } while (0)
+constexpr int kStamps = 8;
+#else
+#define CE_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
+__host__ __device__ constexpr size_t align16(size_t v) { return (v + 15) & ~size_t(15); }
+
+// Row-major dataset rows padded to an odd number of 16-byte units: one row
+// is F/2 (double) or F/4 (float) 16-byte loads at immediate offsets, and the
+// 16 lanes a ds_read_b128 services together hit 16 disjoint 4-bank groups.
+__host__ __device__ constexpr int row_stride(int F, int tsize) {
+    const int units = (F * tsize + 15) / 16;
+    return (units % 2 ? units : units + 1) * 16 / tsize;
+}
+
+// Bytes of the [rows | labels] dataset image (device buffer and LDS stage).
+__host__ __device__ constexpr size_t stage_bytes_total(int F, int N, int tsize) {
+    return align16(align16(static_cast<size_t>(row_stride(F, tsize)) * N * tsize) +
+                   static_cast<size_t>(N) * 4);
+}
+
+template <typename T>
+struct Vec16;
+template <>
+struct Vec16<double> { using type = double2; static constexpr int n = 2; };
+template <>
+struct Vec16<float> { using type = float4; static constexpr int n = 4; };
+
+template <typename T, int F>
+__device__ __forceinline__ void load_row(const T *base, int r, T (&x)[F]) {
+    using V = typename Vec16<T>::type;
+    constexpr int NV = (F + Vec16<T>::n - 1) / Vec16<T>::n;
+    constexpr int RS = row_stride(F, sizeof(T));
+    const V *src = reinterpret_cast<const V *>(base + static_cast<size_t>(r) * RS);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const V q = src[v];
+        const T *qe = reinterpret_cast<const T *>(&q);
+#pragma unroll
+        for (int c = 0; c < Vec16<T>::n; ++c)
+            if (v * Vec16<T>::n + c < F) x[v * Vec16<T>::n + c] = qe[c];
+    }
+}
 
 __device__ __forceinline__ double readlane(double v, int l) {
     const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(v));
@@ -92,7 +186,6 @@ template <typename T, int NP, int OFF>
 struct ReduceScatter {
     static __device__ __forceinline__ void run(T (&acc)[NP], int lane) {
         constexpr int half = NP / 2;
-        static_assert(NP >= 2, "");
         const bool hi = (lane & OFF) != 0;
 #pragma unroll
         for (int j = 0; j < half; ++j) {
@@ -127,45 +220,221 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
-// Forward pass of one row: softmax probabilities, loss term, hit.
+// ---------------------------------------------------------------------------
+// Problem kernels.  Each "Model" describes the per-row math, how many values
+// a lane accumulates (NE gradient elements + loss + hits), and how a reduced
+// element maps back to parameters.
+//
+// General K: the softmax classifier exactly as written in the reference.
 template <typename T, int F, int K>
-__device__ __forceinline__ void row_forward(const T (&x)[F], const T (&w)[F * K], int y,
-                                            T (&p)[K], T &loss_term, int &hit) {
-    T logit[K];
+struct SoftmaxModel {
+    static constexpr int P = F * K;
+    static constexpr int NE = P;           // reduced gradient elements
+    static constexpr int NB = F * K;       // broadcast weight values
+
+    static __device__ __forceinline__ void broadcast(T wl, T (&w)[NB]) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        T s = x[0] * w[k];
-#pragma unroll
-        for (int f = 1; f < F; ++f) s = fma(x[f], w[f * K + k], s);
-        logit[k] = s;
+        for (int j = 0; j < NB; ++j) w[j] = readlane(wl, j);
     }
-    T m = logit[0];
+
+    // Returns the row's loss term and hit; adds x^T (p - y) into acc if grad.
+    template <bool GRAD, bool MASKED, int NA>
+    static __device__ __forceinline__ void row(const T (&x)[F], const T (&w)[NB], int y,
+                                               bool valid, const MathConsts<T> &,
+                                               T (&acc)[NA], T &loss_term, T &hit) {
+        T logit[K];
 #pragma unroll
-    for (int k = 1; k < K; ++k) m = logit[k] > m ? logit[k] : m;
-    T denom = T(0);
+        for (int k = 0; k < K; ++k) {
+            T s = x[0] * w[k];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        p[k] = exp_t(logit[k] - m);
-        denom += p[k];
+            for (int f = 1; f < F; ++f) s = fma(x[f], w[f * K + k], s);
+            logit[k] = s;
+        }
+        T m = logit[0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) m = logit[k] > m ? logit[k] : m;
+        T p[K], denom = T(0);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            p[k] = exp_t(logit[k] - m);
+            denom += p[k];
+        }
+        int best = 0;
+        T py = T(0), rest = T(0);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            p[k] = p[k] / denom;
+            if (k > 0 && p[k] > p[best]) best = k;   // np.argmax: first maximum
+            if (k == y) py = p[k]; else rest += p[k];
+        }
+        valid = valid || !MASKED;
+        loss_term = valid ? -log_t(py + T(1e-16)) : T(0);
+        hit = (valid && best == y) ? T(1) : T(0);
+        if (GRAD) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                T d = (k == y) ? -rest : p[k];         // p_k - y_k
+                d = valid ? d : T(0);
+#pragma unroll
+                for (int f = 0; f < F; ++f) acc[f * K + k] = fma(x[f], d, acc[f * K + k]);
+            }
+        }
     }
-    int best = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        p[k] = p[k] / denom;
-        if (k > 0 && p[k] > p[best]) best = k;   // np.argmax: first maximum
+
+    // Parameter index and sign of the value this lane owns after the reduction.
+    static __device__ __forceinline__ bool param_of(int m, int sub, int &j, T &sign) {
+        j = m;
+        sign = T(1);
+        return sub == 0 && m < P;
     }
-    T py = p[0];
+};
+
+// 1/d for d in [1, 4]: hardware reciprocal + two Newton steps (no scaling
+// or special cases needed on that range; <= 1 ulp).
+__device__ __forceinline__ double rcp_unit(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+__device__ __forceinline__ float rcp_unit(float d) { return __builtin_amdgcn_rcpf(d); }
+
+// exp(-a) for a >= 0:  n = rint(a log2e),  r = n ln2 - a in [-ln2/2, ln2/2],
+// exp(-a) = 2^-n exp(r).
+template <typename T>
+__device__ __forceinline__ T exp_neg(T a, const MathConsts<T> &) {
+    const T n = rint(a * kLog2e);
+    const T r = fma(n, kLn2Lo, fma(n, kLn2Hi, -a));
+    T q = kExpCoef[kExpTerms - 1];
 #pragma unroll
-    for (int k = 1; k < K; ++k) py = (k == y) ? p[k] : py;
-    loss_term = -log_t(py + T(1e-16));
-    hit = (best == y) ? 1 : 0;
+    for (int k = kExpTerms - 2; k >= 0; --k) q = fma(q, r, kExpCoef[k]);
+    const T v = ldexp(q, -static_cast<int>(n));
+    return a < T(700) ? v : T(0);
 }
 
-template <typename T, int F>
-__device__ __forceinline__ void load_row(const T *X, int r, T (&x)[F]) {
-    const T *src = X + static_cast<size_t>(r) * F;
+// log(1 + t) for t in [0, 1]:  1 + t = 2^e m,
+// log1p(t) = e ln2 + 2 atanh(s), s = (m - 1)/(m + 1) in [-0.1716, 0.1716]:
+//   e = 0: s = t / (2 + t)          (keeps full relative accuracy as t -> 0)
+//   e = 1: s = (t - 1) / (t + 3)
+template <typename T>
+__device__ __forceinline__ T log1p_unit(T t, const MathConsts<T> &) {
+    const bool hi = t > T(0.41421356237309503);
+    const T s = (hi ? t - T(1) : t) * rcp_unit(hi ? t + T(3) : t + T(2));
+    const T s2 = s * s;
+    T q = kLogCoef[kLogTerms - 1];
 #pragma unroll
-    for (int f = 0; f < F; ++f) x[f] = src[f];
+    for (int k = kLogTerms - 2; k >= 0; --k) q = fma(q, s2, kLogCoef[k]);
+    return fma(T(2) * s, q, hi ? kLn2Lo : T(0)) + (hi ? kLn2Hi : T(0));
+}
+
+// float32 engine: hardware v_exp_f32 / v_log_f32 (about 1 ulp of float).
+__device__ __forceinline__ float exp_neg(float a, const MathConsts<float> &) {
+    return __expf(-a);
+}
+__device__ __forceinline__ float log1p_unit(float t, const MathConsts<float> &) {
+    return __logf(1.0f + t);
+}
+
+// -log(q) for any positive normal q, inline: q = 2^e m, m in [1, 2),
+// log(m) = log1p(m - 1) with m - 1 exact.  Used for the literal
+// -log(p + 1e-16) of rows whose minority-class probability is tiny.
+__device__ __forceinline__ double neg_log_eps(double p) {
+    const double q = p + 1e-16;
+    const int ex = __builtin_amdgcn_frexp_exp(q) - 1;   // q = 2^ex * m, m in [1, 2)
+    const double m = ldexp(__builtin_amdgcn_frexp_mant(q), 1);
+    const double lm = log1p_unit(m - 1.0, MathConsts<double>());
+    return -(fma(static_cast<double>(ex), kLn2Hi, fma(static_cast<double>(ex), kLn2Lo, lm)));
+}
+__device__ __forceinline__ float neg_log_eps(float p) { return -__logf(p + 1e-16f); }
+
+// K = 2: the same softmax in its two-class form (see file header).
+//   t = exp(-|z|), p_max = 1/(1+t), p_min = t/(1+t)
+//   -log(p_max + 1e-16) = log1p(t)            (p_max >= 1/2: the 1e-16 is
+//                                               below half an ulp of the log)
+//   -log(p_min + 1e-16) = |z| + log1p(t)      when p_min >= 1e-6 (dropping
+//                                               1e-16 moves it < 1e-10)
+//   otherwise the literal -log(p_min + 1e-16) (rare, data-dependent branch).
+template <typename T, int F>
+struct TwoClassModel {
+    static constexpr int K = 2;
+    static constexpr int P = F * 2;
+    static constexpr int NE = F;           // column 1 of the gradient = -column 0
+    static constexpr int NB = F;           // broadcast w0 - w1
+
+    static __device__ __forceinline__ void broadcast(T wl, T (&wd)[NB]) {
+        const T d = wl - __shfl_down(wl, 1);       // lane 2f: w[f][0] - w[f][1]
+#pragma unroll
+        for (int f = 0; f < F; ++f) wd[f] = readlane(d, 2 * f);
+    }
+
+    template <bool GRAD, bool MASKED, int NA>
+    static __device__ __forceinline__ void row(const T (&x)[F], const T (&wd)[NB], int y,
+                                               bool valid, const MathConsts<T> &mc,
+                                               T (&acc)[NA], T &loss_term, T &hit) {
+        T z = x[0] * wd[0];
+#pragma unroll
+        for (int f = 1; f < F; ++f) z = fma(x[f], wd[f], z);
+        const T az = fabs(z);
+        const T t = exp_neg(az, mc);
+        const T inv = rcp_unit(T(1) + t);           // p of the larger-logit class
+        const T lo = t * inv;                       // p of the other class
+        const bool y0 = y == 0;
+        const bool y_is_min = y0 != (z >= T(0));   // class 0 wins ties (z = 0)
+        T lt = log1p_unit(t, mc) + (y_is_min ? az : T(0));
+        const bool tiny = y_is_min && lo < T(1e-6);
+        if (__any(tiny)) {                         // wave-uniform: skipped unless needed
+            if (tiny) lt = neg_log_eps(lo);
+        }
+        // np.argmax(P) == y with first-maximum ties (p equal only if inv == lo)
+        const bool tie = !(inv > lo);
+        const bool hit_b = y0 ? (!y_is_min || tie) : (!y_is_min && !tie);
+        loss_term = MASKED && !valid ? T(0) : lt;
+        hit = (hit_b && (!MASKED || valid)) ? T(1) : T(0);
+        if (GRAD) {
+            // p_0 - y_0 = -(1 - p_y) if y = 0 else p_0: magnitude is the
+            // probability of the class that is not y, sign is - iff y = 0
+            const T mag = y_is_min ? inv : lo;
+            T d0 = y0 ? -mag : mag;
+            if (MASKED) d0 = valid ? d0 : T(0);
+#pragma unroll
+            for (int f = 0; f < F; ++f) acc[f] = fma(x[f], d0, acc[f]);
+        }
+    }
+
+    static __device__ __forceinline__ bool param_of(int m, int sub, int &j, T &sign) {
+        j = 2 * m + sub;
+        sign = sub == 0 ? T(1) : T(-1);
+        return sub < 2 && m < F;
+    }
+};
+
+template <int F, int K>
+struct UseTwoClass { static constexpr bool value = (K == 2) && (F + 2 <= 32); };
+
+// UU chunks of 64 minibatch rows: minibatch row i -> dataset row order[i].
+template <typename Model, typename T, int F, bool MASKED, int UU, int NA>
+__device__ __forceinline__ void rows_block(const T *xs, const int32_t *ys, const int32_t *order,
+                                           int i, int B, const T (&w)[Model::NB],
+                                           const MathConsts<T> &mc, T (&acc)[NA]) {
+    T x[UU][F];
+    int y[UU];
+    bool valid[UU];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const int iu = i + u * kWave;
+        valid[u] = !MASKED || iu < B;
+        const int r = valid[u] ? (order ? order[iu] : iu) : 0;
+        load_row<T, F>(xs, r, x[u]);
+        y[u] = ys[r];
+    }
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        T lt, hit;
+        Model::template row<true, MASKED>(x[u], w, y[u], valid[u], mc, acc, lt, hit);
+        acc[Model::NE] += lt;
+        acc[Model::NE + 1] += hit;
+    }
 }
 
 // Restore the env to what Optimize.base_reset leaves (optimize.py:58-67):
@@ -203,101 +472,144 @@ __global__ __launch_bounds__(kBlock) void optimize_reset_kernel(StepArgs<T> a) {
     for (int i = lane; i < OBS; i += kWave) a.obs[static_cast<size_t>(e) * OBS + i] = 0.0f;
 }
 
-template <typename T, int F, int K>
+template <typename T, int F, int K, bool STAGED>
 __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
+    using Model = typename std::conditional<UseTwoClass<F, K>::value, TwoClassModel<T, F>,
+                                            SoftmaxModel<T, F, K>>::type;
     constexpr int P = F * K;
     constexpr int OBS = 2 * P + 1;
-    constexpr int NP = next_pow2(P + 2);
-    static_assert(NP <= kWave, "register path needs F*K + 2 <= 64");
+    constexpr int NE = Model::NE;
+    constexpr int NP = next_pow2(NE + 2);
+    static_assert(NP <= kWave, "register path needs the reduced set to fit one wave");
     constexpr int SHIFT = 6 - Log2<NP>::value;
 
+#ifdef CE_DIAG
+    unsigned long long stamps[kStamps] = {0};
+    stamps[6] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
+#endif
+    CE_STAMP(0);
     const int lane = threadIdx.x & (kWave - 1);
     const int e = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    if (e >= a.E) return;   // wave-uniform
-    const size_t pbase = static_cast<size_t>(e) * P;
+    const bool active = e < a.E;   // wave-uniform
+    const size_t pbase = static_cast<size_t>(active ? e : 0) * P;
+    const int N = a.N;
+
+    // ---- per-env state loads first: their latency overlaps the staging copy.
+    T wl = T(0), al = T(0);
+    if (active && lane < P) {
+        wl = a.W[pbase + lane];
+        al = static_cast<T>(a.act[pbase + lane]);
+    }
+    int j_own;
+    T sign_own;
+    const bool owner = Model::param_of(lane >> SHIFT, lane & ((1 << SHIFT) - 1), j_own, sign_own);
+    const T gprev = (active && owner) ? a.G[pbase + j_own] : T(0);
+    const double lprev = active ? a.L[e] : 0.0;
+    const int step_prev = active ? a.step[e] : 0;
+
+    // ---- dataset: [rows | labels] staged into LDS once per block (16-byte copies).
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int RS = row_stride(F, sizeof(T));
+    const size_t xbytes = align16(sizeof(T) * RS * static_cast<size_t>(N));
+    const T *xs;
+    const int32_t *ys;
+    if constexpr (STAGED) {
+        const int nvec = static_cast<int>(align16(xbytes + 4 * static_cast<size_t>(N)) / 16);
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.data);
+        uint4 *dst = reinterpret_cast<uint4 *>(smem);
+        // Every block reads the same few KB: rotate each block's starting
+        // vector so the 32 CUs of an XCD do not queue on the same L2 lines
+        // at the same moment; all of a thread's loads go out before the
+        // first LDS write.
+        constexpr int kBatch = 4;
+        const int rot = static_cast<int>((blockIdx.x * 97u) % static_cast<unsigned>(nvec));
+        for (int i0 = threadIdx.x; i0 < nvec; i0 += kBatch * kBlock) {
+            uint4 v[kBatch];
+            int idx[kBatch];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) {
+                const int i = i0 + b * kBlock;
+                idx[b] = i + rot < nvec ? i + rot : i + rot - nvec;
+                if (i < nvec) v[b] = src[idx[b]];
+            }
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b)
+                if (i0 + b * kBlock < nvec) dst[idx[b]] = v[b];
+        }
+        __syncthreads();
+        CE_STAMP(1);
+        xs = reinterpret_cast<const T *>(smem);
+        ys = reinterpret_cast<const int32_t *>(smem + xbytes);
+    } else {
+        xs = reinterpret_cast<const T *>(a.data);
+        ys = reinterpret_cast<const int32_t *>(a.data + xbytes);
+    }
+    if (!active) return;
 
     // ---- W <- W - a (optimize.py:74-75); lane j owns parameter j.
-    T wl = T(0);
-    if (lane < P) wl = a.W[pbase + lane] - static_cast<T>(a.act[pbase + lane]);
-    T w[P];
-#pragma unroll
-    for (int j = 0; j < P; ++j) w[j] = readlane(wl, j);
-    const int cur_step = __builtin_amdgcn_readfirstlane(a.step[e]) + 1;
+    wl = wl - al;
+    T w[Model::NB];
+    Model::broadcast(wl, w);
+    const int cur_step = __builtin_amdgcn_readfirstlane(step_prev) + 1;
+    CE_STAMP(2);
 
     // ---- minibatch rows: sequence[0] = rows [0, B) of the current order.
     const int32_t *order = nullptr;
     if (a.order != nullptr) {
         const int sel = __builtin_amdgcn_readfirstlane(a.order_sel[e]);
-        order = a.order + sel * static_cast<size_t>(a.E) * a.N + static_cast<size_t>(e) * a.N;
+        order = a.order + sel * static_cast<size_t>(a.E) * N + static_cast<size_t>(e) * N;
     }
     T acc[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j) acc[j] = T(0);
-    for (int i0 = 0; i0 < a.B; i0 += kWave) {
-        const int i = i0 + lane;
-        if (i < a.B) {
-            const int r = order ? order[i] : i;
-            T x[F];
-            load_row<T, F>(a.X, r, x);
-            const int y = a.label[r];
-            T p[K], lt;
-            int hit;
-            row_forward<T, F, K>(x, w, y, p, lt, hit);
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const T d = p[k] - (k == y ? T(1) : T(0));
-#pragma unroll
-                for (int f = 0; f < F; ++f) acc[f * K + k] = fma(x[f], d, acc[f * K + k]);
-            }
-            acc[P] += lt;
-            acc[P + 1] += static_cast<T>(hit);
-        }
-    }
+    // Full groups of U chunks (64 rows each) run unmasked with U independent
+    // dependency chains in flight; a ragged tail runs one masked chunk at a time.
+    constexpr int U = sizeof(T) == 8 ? 1 : 4;
+    const int full = a.B / (kWave * U) * (kWave * U);
+    for (int i0 = 0; i0 < full; i0 += kWave * U)
+        rows_block<Model, T, F, false, U>(xs, ys, order, i0 + lane, a.B, w, MathConsts<T>(), acc);
+    for (int i0 = full; i0 < a.B; i0 += kWave)
+        rows_block<Model, T, F, true, 1>(xs, ys, order, i0 + lane, a.B, w, MathConsts<T>(), acc);
+    CE_STAMP(3);
     ReduceScatter<T, NP, 32>::run(acc, lane);
-    const int mine = lane >> SHIFT;              // element this lane now owns
-    const bool owner = (lane & ((1 << SHIFT) - 1)) == 0;
-    const T tot_loss = readlane(acc[0], P << SHIFT);
-    const T tot_hit = readlane(acc[0], (P + 1) << SHIFT);
+    const T tot_loss = readlane(acc[0], NE << SHIFT);
+    const T tot_hit = readlane(acc[0], (NE + 1) << SHIFT);
     const double loss = static_cast<double>(tot_loss) / a.B;
-    const double acc_mb = static_cast<double>(tot_hit) / a.B;
+    double objective = loss, accuracy = static_cast<double>(tot_hit) / a.B;
 
     // ---- info pass over the full dataset (optimize.py:94-97); with B == N
     // the minibatch *is* the dataset and the reference computes the same
     // numbers twice, so they are reused.
-    double objective = loss, accuracy = acc_mb;
-    if (a.B != a.N) {
+    if (a.B != N) {
         T fl = T(0), fh = T(0);
-        for (int i0 = 0; i0 < a.N; i0 += kWave) {
+        T none[1];
+        for (int i0 = 0; i0 < N; i0 += kWave) {
             const int r = i0 + lane;
-            if (r < a.N) {
-                T x[F];
-                load_row<T, F>(a.X, r, x);
-                T p[K], lt;
-                int hit;
-                row_forward<T, F, K>(x, w, a.label[r], p, lt, hit);
-                fl += lt;
-                fh += static_cast<T>(hit);
-            }
+            const bool valid = r < N;
+            const int rr = valid ? r : 0;
+            T x[F];
+            load_row<T, F>(xs, rr, x);
+            T lt, hit;
+            Model::template row<false, true>(x, w, ys[rr], valid, MathConsts<T>(), none, lt, hit);
+            fl += lt;
+            fh += hit;
         }
-        fl = wave_sum(fl);
-        fh = wave_sum(fh);
-        objective = static_cast<double>(fl) / a.N;
-        accuracy = static_cast<double>(fh) / a.N;
+        objective = static_cast<double>(wave_sum(fl)) / N;
+        accuracy = static_cast<double>(wave_sum(fh)) / N;
     }
 
+    CE_STAMP(4);
     // ---- recurrences (optimize.py:80-86) and outputs.
-    const double lprev = a.L[e];
     const double lnew = (loss - lprev) / (lprev + 0.1);
     const bool done = cur_step >= a.max_steps;
     const bool wipe = done && a.auto_reset;   // VecEnv auto-reset this step
     float *obs = a.obs + static_cast<size_t>(e) * OBS;
-    if (owner && mine < P) {
-        const T g = static_cast<T>(static_cast<double>(acc[0]) / a.B);
-        const T gprev = a.G[pbase + mine];
+    if (owner) {
+        const T g = sign_own * acc[0] / static_cast<T>(a.B);
         const T gnew = g / (fabs(gprev) + T(1));
         if (!wipe) {
-            a.G[pbase + mine] = gnew;
-            obs[P + 1 + mine] = static_cast<float>(gnew);
+            a.G[pbase + j_own] = gnew;
+            obs[P + 1 + j_own] = static_cast<float>(gnew);
         }
     }
     if (lane < P) {
@@ -320,6 +632,12 @@ __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
         reset_env<T, P>(a, e, lane);
         for (int i = lane; i < OBS; i += kWave) obs[i] = 0.0f;
     }
+#ifdef CE_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    CE_STAMP(5);
+    stamps[7] = __builtin_amdgcn_s_memrealtime();
+    if (lane < kStamps) a.diag[static_cast<size_t>(e) * kStamps + lane] = stamps[lane];
+#endif
 }
 
 }  // namespace ce

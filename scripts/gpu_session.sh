@@ -16,6 +16,10 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 echo "smoke rc=$rc"; tail -3 $OUT/smoke.log; fatal $rc
 timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?
 echo "bench rc=$rc"; tail -2 $OUT/bench.log; fatal $rc
+if [ -n "${SWEEP:-}" ]; then
+  timeout -k 10 300 python scripts/sweep.py > $OUT/sweep.log 2>&1; rc=$?
+  echo "sweep rc=$rc"; cat $OUT/sweep.log | grep envs; fatal $rc
+fi
 if [ -n "${PROFILE:-}" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --profile-only --steps 2000 --warmup 100 ${BENCH_ARGS:-} > $OUT/prof.log 2>&1; rc=$?
   echo "rocprof rc=$rc"; tail -3 $OUT/prof.log; fatal $rc
