@@ -363,6 +363,8 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         return bail(fail(CE_EHIP, "ce_create: dataset upload failed"));
     e->stage_bytes = ce::stage_bytes_total(cfg->n_features, cfg->n_rows, static_cast<int>(e->tsize));
     e->staged = e->stage_bytes <= ce::kStageLimit;
+    if (const char *ns = std::getenv("CE_NO_STAGE"))   // experiment switch: rows from L1/L2
+        if (ns[0] == '1') e->staged = false;
     // Unseeded envs behave like np_random(None): os.urandom seeds.  The host
     // side normally seeds explicitly; default to seed = env index here.
     std::vector<uint64_t> seeds(E);

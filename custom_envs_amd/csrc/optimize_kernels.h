@@ -179,30 +179,106 @@ constexpr int next_pow2(int v) {
     return p;
 }
 
+// Cross-lane exchange primitives (gfx950).  xchg<OFF> returns the value of
+// lane (l ^ OFF) for OFF < 16 (DPP quad_perm / row_ror:8, ds_swizzle for 4);
+// the 16- and 32-lane levels use v_permlane16/32_swap, which exchange whole
+// register halves between two VGPRs in one instruction.
+template <int OFF>
+__device__ __forceinline__ unsigned xchg_u32(unsigned v) {
+    if constexpr (OFF == 1)
+        return __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    else if constexpr (OFF == 2)
+        return __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    else if constexpr (OFF == 4)
+        return __builtin_amdgcn_ds_swizzle(v, 0x101f);                      // xor 4 (bitmask mode)
+    else
+        return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xf, 0xf, false);  // row_ror:8 = xor 8
+}
+
+template <int OFF>
+__device__ __forceinline__ double xchg(double v) {
+    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+    const unsigned lo = xchg_u32<OFF>(static_cast<unsigned>(b));
+    const unsigned hi = xchg_u32<OFF>(static_cast<unsigned>(b >> 32));
+    return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+}
+template <int OFF>
+__device__ __forceinline__ float xchg(float v) { return __uint_as_float(xchg_u32<OFF>(__float_as_uint(v))); }
+
+// (a, b) -> (a', b') with a' + b' = [A totals | B totals]: for OFF = 32 the
+// lanes with bit 5 clear end up with a_l + a_{l^32}, the others with
+// b_l + b_{l^32}; OFF = 16 likewise on 16-lane rows.
+template <int OFF>
+__device__ __forceinline__ void swap_halves_u32(unsigned &a, unsigned &b) {
+    if constexpr (OFF == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+        a = r[0];
+        b = r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+        a = r[0];
+        b = r[1];
+    }
+}
+template <int OFF>
+__device__ __forceinline__ double fold_pair(double a, double b) {
+    unsigned long long ab = static_cast<unsigned long long>(__double_as_longlong(a));
+    unsigned long long bb = static_cast<unsigned long long>(__double_as_longlong(b));
+    unsigned alo = static_cast<unsigned>(ab), ahi = static_cast<unsigned>(ab >> 32);
+    unsigned blo = static_cast<unsigned>(bb), bhi = static_cast<unsigned>(bb >> 32);
+    swap_halves_u32<OFF>(alo, blo);
+    swap_halves_u32<OFF>(ahi, bhi);
+    const double a2 = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(ahi) << 32) | alo));
+    const double b2 = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(bhi) << 32) | blo));
+    return a2 + b2;
+}
+template <int OFF>
+__device__ __forceinline__ float fold_pair(float a, float b) {
+    unsigned au = __float_as_uint(a), bu = __float_as_uint(b);
+    swap_halves_u32<OFF>(au, bu);
+    return __uint_as_float(au) + __uint_as_float(bu);
+}
+
 // Recursive-halving reduce-scatter over the 64 lanes of a wave.  On entry
 // acc[0..NP) holds per-lane partials; on exit acc[0] of lane l holds the
-// wave total of element (l >> (6 - log2 NP)).
+// wave total of element (l >> (6 - log2 NP)).  Levels 32 and 16 are
+// select-free permlane swaps; lower levels exchange the half a lane gives up.
 template <typename T, int NP, int OFF>
 struct ReduceScatter {
     static __device__ __forceinline__ void run(T (&acc)[NP], int lane) {
         constexpr int half = NP / 2;
-        const bool hi = (lane & OFF) != 0;
+        if constexpr (OFF >= 16) {
 #pragma unroll
-        for (int j = 0; j < half; ++j) {
-            const T keep = hi ? acc[j + half] : acc[j];
-            const T send = hi ? acc[j] : acc[j + half];
-            acc[j] = keep + __shfl_xor(send, OFF);
+            for (int j = 0; j < half; ++j) acc[j] = fold_pair<OFF>(acc[j], acc[j + half]);
+        } else {
+            const bool hi = (lane & OFF) != 0;
+#pragma unroll
+            for (int j = 0; j < half; ++j) {
+                const T keep = hi ? acc[j + half] : acc[j];
+                const T send = hi ? acc[j] : acc[j + half];
+                acc[j] = keep + xchg<OFF>(send);
+            }
         }
         T (&next)[half] = *reinterpret_cast<T(*)[half]>(&acc[0]);
         ReduceScatter<T, half, OFF / 2>::run(next, lane);
     }
 };
+
+// Sum of v over the lanes that differ in bits OFF, OFF/2, ..., 1.
+template <typename T, int OFF>
+__device__ __forceinline__ T lane_sum(T v) {
+    if constexpr (OFF == 0) {
+        return v;
+    } else {
+        if constexpr (OFF >= 16) v = fold_pair<OFF>(v, v);
+        else v = v + xchg<OFF>(v);
+        return lane_sum<T, OFF / 2>(v);
+    }
+}
+
 template <typename T, int OFF>
 struct ReduceScatter<T, 1, OFF> {
-    static __device__ __forceinline__ void run(T (&acc)[1], int) {
-#pragma unroll
-        for (int off = OFF; off >= 1; off >>= 1) acc[0] += __shfl_xor(acc[0], off);
-    }
+    static __device__ __forceinline__ void run(T (&acc)[1], int) { acc[0] = lane_sum<T, OFF>(acc[0]); }
 };
 template <typename T, int NP>
 struct ReduceScatter<T, NP, 0> {
@@ -214,11 +290,7 @@ struct ReduceScatter<T, 1, 0> {
 };
 
 template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
+__device__ __forceinline__ T wave_sum(T v) { return lane_sum<T, 32>(v); }
 
 // ---------------------------------------------------------------------------
 // Problem kernels.  Each "Model" describes the per-row math, how many values
@@ -287,6 +359,8 @@ struct SoftmaxModel {
         sign = T(1);
         return sub == 0 && m < P;
     }
+    // A lane that owns parameter j after a reduction with the given shift.
+    static __device__ __forceinline__ int owner_lane(int j, int shift) { return j << shift; }
 };
 
 // 1/d for d in [1, 4]: hardware reciprocal + two Newton steps (no scaling
@@ -406,6 +480,9 @@ struct TwoClassModel {
         j = 2 * m + sub;
         sign = sub == 0 ? T(1) : T(-1);
         return sub < 2 && m < F;
+    }
+    static __device__ __forceinline__ int owner_lane(int j, int shift) {
+        return ((j >> 1) << shift) | (j & 1);
     }
 };
 
@@ -604,17 +681,24 @@ __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
     const bool done = cur_step >= a.max_steps;
     const bool wipe = done && a.auto_reset;   // VecEnv auto-reset this step
     float *obs = a.obs + static_cast<size_t>(e) * OBS;
+    float gnew_f = 0.0f;
     if (owner) {
         const T g = sign_own * acc[0] / static_cast<T>(a.B);
         const T gnew = g / (fabs(gprev) + T(1));
-        if (!wipe) {
-            a.G[pbase + j_own] = gnew;
-            obs[P + 1 + j_own] = static_cast<float>(gnew);
-        }
+        if (!wipe) a.G[pbase + j_own] = gnew;
+        gnew_f = static_cast<float>(gnew);
     }
-    if (lane < P) {
-        obs[lane] = 0.0f;
-        if (!wipe) a.W[pbase + lane] = wl;
+    if (lane < P && !wipe) a.W[pbase + lane] = wl;
+    // obs row = [0 (P) | L' | G' (P)], or the zero reset obs: one coalesced
+    // store per 64 entries, G' gathered from its owner lanes.
+#pragma unroll
+    for (int i0 = 0; i0 < OBS; i0 += kWave) {
+        const int i = i0 + lane;
+        const int src = (i > P && i < OBS) ? Model::owner_lane(i - P - 1, SHIFT) : 0;
+        const float gv = __shfl(gnew_f, src);
+        float v = i < P ? 0.0f : (i == P ? static_cast<float>(lnew) : gv);
+        if (wipe) v = 0.0f;
+        if (i < OBS) obs[i] = v;
     }
     if (lane == 0) {
         a.reward[e] = static_cast<float>(-loss);
@@ -625,13 +709,9 @@ __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
         if (!wipe) {
             a.L[e] = lnew;
             a.step[e] = cur_step;
-            obs[P] = static_cast<float>(lnew);
         }
     }
-    if (wipe) {   // the returned obs is the reset obs (zeros)
-        reset_env<T, P>(a, e, lane);
-        for (int i = lane; i < OBS; i += kWave) obs[i] = 0.0f;
-    }
+    if (wipe) reset_env<T, P>(a, e, lane);   // the returned obs was the reset obs (zeros)
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     CE_STAMP(5);
