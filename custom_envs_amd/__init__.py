@@ -10,6 +10,7 @@ from custom_envs_amd.data import load_data
 from custom_envs_amd._native import NativeEngineError
 
 register(id='Optimize-v0', entry_point='custom_envs_amd.envs.optimize:Optimize')
+register(id='MultiOptLRs-v0', entry_point='custom_envs_amd.envs.multioptlrs:MultiOptLRs')
 
 __all__ = ['Env', 'Wrapper', 'make', 'register', 'registry', 'load_data',
            'NativeEngineError']

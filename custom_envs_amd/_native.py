@@ -27,7 +27,16 @@ EXPORTS = (
     'ce_num_envs', 'ce_obs_dim', 'ce_act_dim', 'ce_seed', 'ce_seed_draws', 'ce_reset',
     'ce_step', 'ce_step_async', 'ce_wait', 'ce_step_many', 'ce_host_outputs',
     'ce_get_state', 'ce_set_state',
+    'ce_multi_create', 'ce_multi_destroy', 'ce_multi_set_stream', 'ce_multi_reset',
+    'ce_multi_step', 'ce_multi_step_async', 'ce_multi_wait', 'ce_multi_step_many',
+    'ce_multi_host_outputs', 'ce_multi_get_state',
 )
+
+CE_FUNC_ROSENBROCK_PAIRS = 0
+CE_MULTI_MAX_PARAMS = 16
+MULTI_INFO_KEYS = ('loss', 'batch_loss', 'weights_mean', 'weights_sum', 'actions_mean',
+                   'actions_std', 'states_mean', 'states_sum', 'grads_mean', 'grads_sum',
+                   'loss_mean', 'adjusted_loss', 'adjusted_grad', 'grad_diff')
 
 
 class NativeEngineError(RuntimeError):
@@ -44,6 +53,18 @@ class CeOutputs(ctypes.Structure):
     _fields_ = [('obs', ctypes.c_void_p), ('reward', ctypes.c_void_p),
                 ('done', ctypes.c_void_p), ('objective', ctypes.c_void_p),
                 ('accuracy', ctypes.c_void_p), ('episode_len', ctypes.c_void_p)]
+
+
+class CeMultiConfig(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_int32) for name in (
+        'abi_version', 'device', 'num_envs', 'n_params', 'function', 'max_history',
+        'max_batches', 'auto_reset')] + [('initial_points', ctypes.c_float * 16)]
+
+
+class CeMultiOutputs(ctypes.Structure):
+    _fields_ = [('obs', ctypes.c_void_p), ('reward', ctypes.c_void_p),
+                ('done', ctypes.c_void_p), ('info', ctypes.c_void_p),
+                ('episode_len', ctypes.c_void_p)]
 
 
 class CeState(ctypes.Structure):
@@ -76,6 +97,16 @@ def _declare(lib):
         'ce_host_outputs': ([vp, ctypes.POINTER(CeOutputs)], ctypes.c_int),
         'ce_get_state': ([vp, ctypes.POINTER(CeState)], ctypes.c_int),
         'ce_set_state': ([vp, ctypes.POINTER(CeState)], ctypes.c_int),
+        'ce_multi_create': ([ctypes.POINTER(CeMultiConfig), ctypes.POINTER(vp)], ctypes.c_int),
+        'ce_multi_destroy': ([vp], None),
+        'ce_multi_set_stream': ([vp, vp], ctypes.c_int),
+        'ce_multi_reset': ([vp, ctypes.POINTER(CeMultiOutputs), u32], ctypes.c_int),
+        'ce_multi_step': ([vp, vp, ctypes.POINTER(CeMultiOutputs), u32], ctypes.c_int),
+        'ce_multi_step_async': ([vp, vp, ctypes.POINTER(CeMultiOutputs), u32], ctypes.c_int),
+        'ce_multi_wait': ([vp], ctypes.c_int),
+        'ce_multi_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
+        'ce_multi_host_outputs': ([vp, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
+        'ce_multi_get_state': ([vp, vp, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

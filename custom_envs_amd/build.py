@@ -28,11 +28,12 @@ def _hipcc():
 
 
 def sources():
-    return [os.path.join(CSRC, f) for f in ('engine.hip', 'seeding.cpp')]
+    return [os.path.join(CSRC, f) for f in ('engine.hip', 'multi_engine.hip', 'seeding.cpp')]
 
 
 def headers():
-    return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'seeding.h')] + [
+    return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'multiopt_kernels.h',
+                                            'common.h', 'seeding.h')] + [
         os.path.join(ROOT, 'include', 'custom_envs_amd.h')]
 
 

@@ -17,26 +17,13 @@
 #include <string>
 #include <vector>
 
-#include "../../include/custom_envs_amd.h"
+#include "common.h"
 #include "optimize_kernels.h"
 #include "seeding.h"
 
 namespace {
 
-thread_local std::string g_last_error;
-
-int fail(int code, const std::string &msg) {
-    g_last_error = msg;
-    return code;
-}
-
-#define CE_HIP(call)                                                            \
-    do {                                                                        \
-        hipError_t err_ = (call);                                               \
-        if (err_ != hipSuccess)                                                 \
-            return fail(CE_EHIP, std::string(#call " failed: ") +               \
-                                     hipGetErrorString(err_));                  \
-    } while (0)
+using ce::fail;
 
 using StepFn = void (*)(const void *args, int grid, size_t lds, hipStream_t stream);
 
@@ -76,7 +63,6 @@ const KernelEntry *find_kernel(int precision, int F, int K) {
     return nullptr;
 }
 
-size_t align16(size_t v) { return (v + 15) & ~static_cast<size_t>(15); }
 
 }  // namespace
 
@@ -247,7 +233,7 @@ extern "C" {
 
 int ce_abi_version(void) { return CE_ABI_VERSION; }
 
-const char *ce_last_error(void) { return g_last_error.c_str(); }
+const char *ce_last_error(void) { return ce::last_error().c_str(); }
 
 int ce_seed_draws(uint64_t seed, int32_t n_features, int32_t n_classes, int32_t n_rows,
                   double *init_weights, int32_t *perm) {
@@ -329,7 +315,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
                              E * sizeof(float), E * sizeof(int32_t), E};
     for (int i = 0; i < 6; ++i) {
         e->off[i] = off;
-        off = align16(off + sizes[i]);
+        off = ce::align16(off + sizes[i]);
     }
     e->out_bytes = off;
     CE_TRY(hipMalloc(&e->d_out, e->out_bytes));

@@ -1,0 +1,340 @@
+// C-ABI implementation of the MultiOptLRs-v0 engine (ce_multi_* in
+// include/custom_envs_amd.h).  Same conventions as engine.hip: the engine
+// owns the struct-of-arrays state; host mode stages actions/outputs through
+// pinned buffers and synchronises; CE_PTR_DEVICE calls are stream-ordered.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "multiopt_kernels.h"
+
+namespace {
+
+using ce::fail;
+
+using MultiFn = void (*)(const ce::MultiArgs &, int grid, hipStream_t);
+
+template <int P>
+void launch_multi_step(const ce::MultiArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(ce::multi_step_kernel<P>, dim3(grid), dim3(ce::kMultiBlock), 0, s, a);
+}
+template <int P>
+void launch_multi_reset(const ce::MultiArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(ce::multi_reset_kernel<P>, dim3(grid), dim3(ce::kMultiBlock), 0, s, a);
+}
+
+struct MultiEntry {
+    int P;
+    MultiFn step, reset;
+};
+
+#define CE_MULTI_ENTRY(P) {P, launch_multi_step<P>, launch_multi_reset<P>},
+const MultiEntry kMulti[] = {CE_MULTI_ENTRY(2) CE_MULTI_ENTRY(4) CE_MULTI_ENTRY(6)
+                                 CE_MULTI_ENTRY(8) CE_MULTI_ENTRY(10) CE_MULTI_ENTRY(12)
+                                     CE_MULTI_ENTRY(16)};
+
+}  // namespace
+
+struct ce_multi_engine {
+    ce_multi_config cfg{};
+    const MultiEntry *kern = nullptr;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    float *init = nullptr;
+    int32_t *row_agent = nullptr;
+    float *theta = nullptr, *grad = nullptr, *hl = nullptr, *hg = nullptr, *hw = nullptr;
+    double *al = nullptr, *ag = nullptr, *aw = nullptr;
+    int32_t *step = nullptr;
+    float *d_act = nullptr, *h_act = nullptr;
+    size_t off[5] = {0};
+    size_t out_bytes = 0;
+    char *d_out = nullptr, *h_out = nullptr;
+    bool was_reset = false;
+    hipGraphExec_t graph = nullptr;
+    int graph_k = 0;
+    const float *graph_act = nullptr;
+    int64_t graph_stride = 0;
+    ce_multi_outputs graph_out{};
+    hipStream_t graph_stream = nullptr;
+};
+
+namespace {
+
+ce_multi_outputs region(const ce_multi_engine *e, char *base) {
+    ce_multi_outputs o;
+    o.obs = reinterpret_cast<float *>(base + e->off[0]);
+    o.reward = reinterpret_cast<float *>(base + e->off[1]);
+    o.info = reinterpret_cast<float *>(base + e->off[2]);
+    o.episode_len = reinterpret_cast<int32_t *>(base + e->off[3]);
+    o.done = reinterpret_cast<uint8_t *>(base + e->off[4]);
+    return o;
+}
+
+ce::MultiArgs make_args(const ce_multi_engine *e, const float *act, const ce_multi_outputs &o) {
+    ce::MultiArgs a;
+    a.E = e->cfg.num_envs;
+    a.H = e->cfg.max_history;
+    a.max_batches = e->cfg.max_batches;
+    a.auto_reset = e->cfg.auto_reset;
+    a.init = e->init;
+    a.row_agent = e->row_agent;
+    a.theta = e->theta;
+    a.grad = e->grad;
+    a.hl = e->hl;
+    a.hg = e->hg;
+    a.hw = e->hw;
+    a.al = e->al;
+    a.ag = e->ag;
+    a.aw = e->aw;
+    a.step = e->step;
+    a.act = act;
+    a.obs = o.obs;
+    a.reward = o.reward;
+    a.done = o.done;
+    a.info = o.info;
+    a.episode_len = o.episode_len;
+    return a;
+}
+
+int grid_of(const ce_multi_engine *e) {
+    return (e->cfg.num_envs + ce::kMultiBlock - 1) / ce::kMultiBlock;
+}
+
+bool complete(const ce_multi_outputs *o) {
+    return o && o->obs && o->reward && o->done && o->info && o->episode_len;
+}
+
+void copy_out(const ce_multi_engine *e, const ce_multi_outputs &src, const ce_multi_outputs *dst) {
+    if (!dst) return;
+    const size_t E = e->cfg.num_envs, P = e->cfg.n_params, H = e->cfg.max_history;
+    if (dst->obs) std::memcpy(dst->obs, src.obs, E * P * 3 * H * sizeof(float));
+    if (dst->reward) std::memcpy(dst->reward, src.reward, E * P * sizeof(float));
+    if (dst->done) std::memcpy(dst->done, src.done, E * P);
+    if (dst->info) std::memcpy(dst->info, src.info, E * CE_MULTI_INFO * sizeof(float));
+    if (dst->episode_len) std::memcpy(dst->episode_len, src.episode_len, E * sizeof(int32_t));
+}
+
+int do_step(ce_multi_engine *e, const float *actions, const ce_multi_outputs *out,
+            uint32_t flags, bool sync) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    if (!e->was_reset) return fail(CE_ESTATE, "step() before the first reset()");
+    if (!actions) return fail(CE_EINVAL, "null actions");
+    const size_t rows = static_cast<size_t>(e->cfg.num_envs) * e->cfg.n_params;
+    if (flags & CE_PTR_DEVICE) {
+        if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+        const ce_multi_outputs o = out ? *out : region(e, e->d_out);
+        e->kern->step(make_args(e, actions, o), grid_of(e), e->stream);
+        CE_HIP(hipGetLastError());
+        if (sync) CE_HIP(hipStreamSynchronize(e->stream));
+        return CE_OK;
+    }
+    std::memcpy(e->h_act, actions, rows * sizeof(float));
+    CE_HIP(hipMemcpyAsync(e->d_act, e->h_act, rows * sizeof(float), hipMemcpyHostToDevice,
+                          e->stream));
+    e->kern->step(make_args(e, e->d_act, region(e, e->d_out)), grid_of(e), e->stream);
+    CE_HIP(hipGetLastError());
+    CE_HIP(hipMemcpyAsync(e->h_out, e->d_out, e->out_bytes, hipMemcpyDeviceToHost, e->stream));
+    if (sync) {
+        CE_HIP(hipStreamSynchronize(e->stream));
+        copy_out(e, region(e, e->h_out), out);
+    }
+    return CE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out) {
+    if (!cfg || !out) return fail(CE_EINVAL, "ce_multi_create: null argument");
+    *out = nullptr;
+    if (cfg->abi_version != CE_ABI_VERSION)
+        return fail(CE_EINVAL, "ce_multi_create: ABI version mismatch");
+    if (cfg->function != CE_FUNC_ROSENBROCK_PAIRS)
+        return fail(CE_EUNSUPPORTED, "ce_multi_create: unknown function");
+    if (cfg->num_envs <= 0 || cfg->max_history <= 0 || cfg->max_batches <= 0)
+        return fail(CE_EINVAL, "ce_multi_create: sizes must be positive");
+    if (cfg->n_params < 2 || cfg->n_params % 2 || cfg->n_params > CE_MULTI_MAX_PARAMS)
+        return fail(CE_EINVAL, "ce_multi_create: n_params must be even, 2..16");
+    const MultiEntry *kern = nullptr;
+    for (const auto &k : kMulti)
+        if (k.P == cfg->n_params) kern = &k;
+    if (!kern)
+        return fail(CE_EUNSUPPORTED, "ce_multi_create: no kernel for n_params=" +
+                                         std::to_string(cfg->n_params));
+    ce_multi_engine *e = new (std::nothrow) ce_multi_engine();
+    if (!e) return fail(CE_ENOMEM, "ce_multi_create: host allocation failed");
+    e->cfg = *cfg;
+    e->kern = kern;
+    auto bail = [&](int code) {
+        ce_multi_destroy(e);
+        return code;
+    };
+#define CE_TRY(call)                                                           \
+    do {                                                                       \
+        hipError_t err_ = (call);                                              \
+        if (err_ != hipSuccess)                                                \
+            return bail(fail(CE_EHIP, std::string(#call " failed: ") +         \
+                                          hipGetErrorString(err_)));           \
+    } while (0)
+    CE_TRY(hipSetDevice(cfg->device));
+    CE_TRY(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+    e->stream = e->own_stream;
+    const size_t E = cfg->num_envs, P = cfg->n_params, H = cfg->max_history;
+    CE_TRY(hipMalloc(&e->init, P * sizeof(float)));
+    CE_TRY(hipMalloc(&e->row_agent, P * sizeof(int32_t)));
+    CE_TRY(hipMalloc(&e->theta, P * E * sizeof(float)));
+    CE_TRY(hipMalloc(&e->grad, P * E * sizeof(float)));
+    CE_TRY(hipMalloc(&e->hl, ce::kRawHist * E * sizeof(float)));
+    CE_TRY(hipMalloc(&e->hg, ce::kRawHist * P * E * sizeof(float)));
+    CE_TRY(hipMalloc(&e->hw, ce::kRawHist * P * E * sizeof(float)));
+    CE_TRY(hipMalloc(&e->al, H * E * sizeof(double)));
+    CE_TRY(hipMalloc(&e->ag, H * P * E * sizeof(double)));
+    CE_TRY(hipMalloc(&e->aw, H * P * E * sizeof(double)));
+    CE_TRY(hipMalloc(&e->step, E * sizeof(int32_t)));
+    CE_TRY(hipMalloc(&e->d_act, E * P * sizeof(float)));
+    CE_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_act), E * P * sizeof(float)));
+    const size_t sizes[5] = {E * P * 3 * H * sizeof(float), E * P * sizeof(float),
+                             E * CE_MULTI_INFO * sizeof(float), E * sizeof(int32_t), E * P};
+    size_t off = 0;
+    for (int i = 0; i < 5; ++i) {
+        e->off[i] = off;
+        off = ce::align16(off + sizes[i]);
+    }
+    e->out_bytes = off;
+    CE_TRY(hipMalloc(&e->d_out, e->out_bytes));
+    CE_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_out), e->out_bytes));
+    CE_TRY(hipMemset(e->d_out, 0, e->out_bytes));
+    std::memset(e->h_out, 0, e->out_bytes);
+    // OptEnvRunner rows: agent names sorted as strings (optvecenv.py:10-14,22-23)
+    std::vector<std::string> names(P);
+    for (size_t i = 0; i < P; ++i) names[i] = "parameter-" + std::to_string(i);
+    std::vector<int32_t> order(P);
+    for (size_t i = 0; i < P; ++i) order[i] = static_cast<int32_t>(i);
+    std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return names[x] < names[y]; });
+    CE_TRY(hipMemcpy(e->row_agent, order.data(), P * sizeof(int32_t), hipMemcpyHostToDevice));
+    CE_TRY(hipMemcpy(e->init, cfg->initial_points, P * sizeof(float), hipMemcpyHostToDevice));
+#undef CE_TRY
+    *out = e;
+    return CE_OK;
+}
+
+void ce_multi_destroy(ce_multi_engine *e) {
+    if (!e) return;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->graph) (void)hipGraphExecDestroy(e->graph);
+    void *dev[] = {e->init, e->row_agent, e->theta, e->grad, e->hl, e->hg, e->hw,
+                   e->al, e->ag, e->aw, e->step, e->d_act, e->d_out};
+    for (void *p : dev)
+        if (p) (void)hipFree(p);
+    if (e->h_out) (void)hipHostFree(e->h_out);
+    if (e->h_act) (void)hipHostFree(e->h_act);
+    if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+    delete e;
+}
+
+int ce_multi_set_stream(ce_multi_engine *e, void *stream) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    e->stream = stream ? static_cast<hipStream_t>(stream) : e->own_stream;
+    return CE_OK;
+}
+
+int ce_multi_reset(ce_multi_engine *e, const ce_multi_outputs *out, uint32_t flags) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    if (flags & CE_PTR_DEVICE) {
+        if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+        const ce_multi_outputs o = out ? *out : region(e, e->d_out);
+        e->kern->reset(make_args(e, nullptr, o), grid_of(e), e->stream);
+        CE_HIP(hipGetLastError());
+        e->was_reset = true;
+        return CE_OK;
+    }
+    e->kern->reset(make_args(e, nullptr, region(e, e->d_out)), grid_of(e), e->stream);
+    CE_HIP(hipGetLastError());
+    CE_HIP(hipMemcpyAsync(e->h_out, e->d_out, e->out_bytes, hipMemcpyDeviceToHost, e->stream));
+    CE_HIP(hipStreamSynchronize(e->stream));
+    e->was_reset = true;
+    if (out && out->obs) {
+        const size_t n = static_cast<size_t>(e->cfg.num_envs) * e->cfg.n_params * 3 *
+                         e->cfg.max_history;
+        std::memcpy(out->obs, region(e, e->h_out).obs, n * sizeof(float));
+    }
+    return CE_OK;
+}
+
+int ce_multi_step(ce_multi_engine *e, const float *actions, const ce_multi_outputs *out,
+                  uint32_t flags) {
+    return do_step(e, actions, out, flags, true);
+}
+
+int ce_multi_step_async(ce_multi_engine *e, const float *actions, const ce_multi_outputs *out,
+                        uint32_t flags) {
+    return do_step(e, actions, out, flags, false);
+}
+
+int ce_multi_wait(ce_multi_engine *e) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    CE_HIP(hipStreamSynchronize(e->stream));
+    return CE_OK;
+}
+
+int ce_multi_step_many(ce_multi_engine *e, int32_t k, const float *actions, int64_t stride,
+                       const ce_multi_outputs *out) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
+    if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "bad arguments");
+    if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+    const ce_multi_outputs o = out ? *out : region(e, e->d_out);
+    const bool hit = e->graph && e->graph_k == k && e->graph_act == actions &&
+                     e->graph_stride == stride && e->graph_stream == e->stream &&
+                     std::memcmp(&e->graph_out, &o, sizeof(o)) == 0;
+    if (!hit) {
+        if (e->graph) {
+            CE_HIP(hipGraphExecDestroy(e->graph));
+            e->graph = nullptr;
+        }
+        hipGraph_t g;
+        CE_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+        for (int s = 0; s < k; ++s)
+            e->kern->step(make_args(e, actions + s * stride, o), grid_of(e), e->stream);
+        CE_HIP(hipStreamEndCapture(e->stream, &g));
+        hipError_t err = hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (err != hipSuccess)
+            return fail(CE_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(err));
+        e->graph_k = k;
+        e->graph_act = actions;
+        e->graph_stride = stride;
+        e->graph_out = o;
+        e->graph_stream = e->stream;
+    }
+    CE_HIP(hipGraphLaunch(e->graph, e->stream));
+    return CE_OK;
+}
+
+int ce_multi_host_outputs(ce_multi_engine *e, ce_multi_outputs *view) {
+    if (!e || !view) return fail(CE_EINVAL, "null argument");
+    *view = region(e, e->h_out);
+    return CE_OK;
+}
+
+int ce_multi_get_state(ce_multi_engine *e, float *theta, int32_t *step) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    const size_t E = e->cfg.num_envs, P = e->cfg.n_params;
+    CE_HIP(hipStreamSynchronize(e->stream));
+    if (theta) {
+        std::vector<float> soa(P * E);
+        CE_HIP(hipMemcpy(soa.data(), e->theta, P * E * sizeof(float), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < E; ++i)
+            for (size_t p = 0; p < P; ++p) theta[i * P + p] = soa[p * E + i];
+    }
+    if (step) CE_HIP(hipMemcpy(step, e->step, E * sizeof(int32_t), hipMemcpyDeviceToHost));
+    return CE_OK;
+}
+
+}  // extern "C"

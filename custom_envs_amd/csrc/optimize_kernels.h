@@ -111,7 +111,7 @@ constexpr int kStamps = 8;
     } while (0)
 #endif
 
-__host__ __device__ constexpr size_t align16(size_t v) { return (v + 15) & ~size_t(15); }
+__host__ __device__ constexpr size_t align16_dev(size_t v) { return (v + 15) & ~size_t(15); }
 
 // Row-major dataset rows padded to an odd number of 16-byte units: one row
 // is F/2 (double) or F/4 (float) 16-byte loads at immediate offsets, and the
@@ -123,7 +123,7 @@ __host__ __device__ constexpr int row_stride(int F, int tsize) {
 
 // Bytes of the [rows | labels] dataset image (device buffer and LDS stage).
 __host__ __device__ constexpr size_t stage_bytes_total(int F, int N, int tsize) {
-    return align16(align16(static_cast<size_t>(row_stride(F, tsize)) * N * tsize) +
+    return align16_dev(align16_dev(static_cast<size_t>(row_stride(F, tsize)) * N * tsize) +
                    static_cast<size_t>(N) * 4);
 }
 
@@ -587,11 +587,11 @@ __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
     // ---- dataset: [rows | labels] staged into LDS once per block (16-byte copies).
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int RS = row_stride(F, sizeof(T));
-    const size_t xbytes = align16(sizeof(T) * RS * static_cast<size_t>(N));
+    const size_t xbytes = align16_dev(sizeof(T) * RS * static_cast<size_t>(N));
     const T *xs;
     const int32_t *ys;
     if constexpr (STAGED) {
-        const int nvec = static_cast<int>(align16(xbytes + 4 * static_cast<size_t>(N)) / 16);
+        const int nvec = static_cast<int>(align16_dev(xbytes + 4 * static_cast<size_t>(N)) / 16);
         const uint4 *src = reinterpret_cast<const uint4 *>(a.data);
         uint4 *dst = reinterpret_cast<uint4 *>(smem);
         // Every block reads the same few KB: rotate each block's starting

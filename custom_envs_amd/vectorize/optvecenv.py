@@ -1,0 +1,282 @@
+"""``OptVecEnv``: multi-agent envs flattened to one VecEnv row per agent.
+
+Reference: custom_envs/vectorize/optvecenv.py:10-91.  ``OptVecEnv(
+environment_fns, callbacks=())`` keeps its constructor, ``agent_no_list``,
+``num_envs = sum of agents``, per-agent spaces, rows in sorted agent-name
+order, reward/done/info replicated per agent, and ``callbacks(states,
+rewards, terminals, infos)`` after each step.
+
+Engine path: when every factory builds the same MultiOptLRs-v0 spec --
+``partial(make, 'MultiOptLRs-v0', **kw)``, ``partial(MultiOptLRs, **kw)``,
+or the scripts' ``partial(Monitor, make(...), log_path, ...)`` (run_multiagent_
+exp_single.py:78-86) -- all envs run in ONE fused kernel per step and the
+Monitors become one ``VecMonitor``.  Anything else runs the reference's
+host path: one worker thread per env around an ``OptEnvRunner``.
+"""
+import functools
+
+import numpy as np
+
+from custom_envs_amd.spaces import Box
+from custom_envs_amd.vectorize.concurrent import ThreadVecEnv
+
+
+def flatten_dictionary(dictionary):
+    """Values of a per-agent dict in sorted-name order (optvecenv.py:10-14)."""
+    return [dictionary[name] for name in sorted(dictionary)]
+
+
+class OptEnvRunner:
+    """One multi-agent env seen as rows (optvecenv.py:17-54)."""
+
+    def __init__(self, environment_fn):
+        env = environment_fn()
+        self._environment = env
+        self._names = sorted(env.action_space.spaces)
+        first = self._names[0]
+        self.observation_space = env.observation_space.spaces[first]
+        self.action_space = env.action_space.spaces[first]
+        self._num_agents = len(env.observation_space.spaces)
+
+    def reset(self):
+        return flatten_dictionary(self._environment.reset())
+
+    def step(self, actions):
+        states, reward, terminal, info = self._environment.step(
+            dict(zip(self._names, actions)))
+        n = self._num_agents
+        return flatten_dictionary(states), [reward] * n, [terminal] * n, [info] * n
+
+    def close(self):
+        self._environment.close()
+
+    def __getattr__(self, attr):
+        if attr.startswith('_'):
+            raise AttributeError(attr)
+        return getattr(self._environment, attr)
+
+
+def _env_spec(obj):
+    """MultiOptLRs kwargs an object or factory stands for, else None."""
+    from custom_envs_amd.core import make
+    from custom_envs_amd.envs.multioptlrs import MultiOptLRs
+    if isinstance(obj, MultiOptLRs):
+        return dict(obj.spec_kwargs), obj
+    if isinstance(obj, functools.partial):
+        if obj.func is make and obj.args == ('MultiOptLRs-v0',):
+            return dict(obj.keywords), None
+        if obj.func is MultiOptLRs and not obj.args:
+            return dict(obj.keywords), None
+    return None
+
+
+def _batch_request(environment_fns):
+    """(env kwargs, monitor settings or None, built envs to close) or None."""
+    from custom_envs_amd.utils.utils_logging import Monitor
+    specs, monitors, built = [], [], []
+    for fn in environment_fns:
+        monitor = None
+        target = fn
+        if isinstance(fn, functools.partial) and fn.func is Monitor:
+            if not fn.args:
+                return None
+            target = fn.args[0]
+            kw = dict(fn.keywords)
+            path = fn.args[1] if len(fn.args) > 1 else kw.pop('file_path', None)
+            kw.pop('allow_early_resets', None)   # run_multiagent_exp_single.py:80
+            monitor = (path, kw)
+        spec = _env_spec(target)
+        if spec is None:
+            return None
+        kwargs, instance = spec
+        specs.append(tuple(sorted((k, tuple(v) if isinstance(v, list) else v)
+                                  for k, v in kwargs.items())))
+        monitors.append(monitor)
+        if instance is not None:
+            built.append(instance)
+    if len(set(specs)) != 1:
+        return None
+    if any(m is None for m in monitors) and any(m is not None for m in monitors):
+        return None
+    mon = None
+    if monitors[0] is not None:
+        if len({repr(sorted(m[1].items())) for m in monitors}) != 1:
+            return None
+        mon = ([m[0] for m in monitors], dict(monitors[0][1]))
+    return dict(specs[0]), mon, built
+
+
+class _RowInfos:
+    """Per-row info dicts, one dict object per env shared by its agent rows."""
+
+    def __init__(self, info, rewards, dones, lengths, n_agents, episodes):
+        self._info, self._rewards, self._dones = info, rewards, dones
+        self._lengths, self._n = lengths, n_agents
+        self._episodes = episodes
+        self._cache = {}
+
+    def env_info(self, env):
+        if env not in self._cache:
+            from custom_envs_amd.envs.multioptlrs import info_dict
+            d = info_dict(self._info[env], bool(self._dones[env]), float(self._rewards[env]),
+                          int(self._lengths[env]))
+            if env in self._episodes:
+                d['episode'] = self._episodes[env]
+            self._cache[env] = d
+        return self._cache[env]
+
+    def per_env(self):
+        """Indexable view: env index -> that env's info dict."""
+        rows = self
+
+        class _View:
+            def __getitem__(self, env):
+                return rows.env_info(env)
+
+            def __len__(self):
+                return len(rows._info)
+        return _View()
+
+    def __len__(self):
+        return len(self._info) * self._n
+
+    def __getitem__(self, row):
+        if isinstance(row, slice):
+            return [self[r] for r in range(*row.indices(len(self)))]
+        if row < 0:
+            row += len(self)
+        return self.env_info(row // self._n)
+
+    def __iter__(self):
+        return (self[r] for r in range(len(self)))
+
+
+class OptVecEnv:
+    def __init__(self, environment_fns, callbacks=()):
+        self.callbacks = callbacks
+        self.closed = False
+        self.waiting = False
+        request = _batch_request(environment_fns)
+        self._engine = self._host = self.monitor = None
+        if request is not None:
+            from custom_envs_amd.multi_engine import MultiOptEngine
+            from custom_envs_amd.utils.utils_logging import VecMonitor
+            kwargs, mon, built = request
+            for env in built:      # single-env engines the caller built eagerly
+                env.close()
+            E = len(environment_fns)
+            self._engine = MultiOptEngine(E, **kwargs)
+            P, H = self._engine.n_params, self._engine.max_history
+            self.agent_no_list = [P] * E
+            self.observation_space = Box(low=-1e6, high=1e6, dtype=np.float32, shape=(3 * H,))
+            self.action_space = Box(low=-1e3, high=1e4, dtype=np.float32, shape=(1,))
+            if mon is not None:
+                paths, mkw = mon
+                self.monitor = VecMonitor(E, paths, info_keywords=mkw.get('info_keywords', ()),
+                                          chunk_size=mkw.get('chunk_size', 1),
+                                          callbacks=mkw.get('callbacks'))
+        else:
+            runners = [functools.partial(OptEnvRunner, fn) for fn in environment_fns]
+            self._host = ThreadVecEnv(runners)
+            self.observation_space = self._host.observation_space
+            self.action_space = self._host.action_space
+            self.agent_no_list = self._host.get_attr('_num_agents')
+        self.num_envs = sum(self.agent_no_list)
+
+    @property
+    def engine_backed(self):
+        return self._engine is not None
+
+    def step_async(self, actions):
+        self.waiting = True
+        if self._engine is not None:
+            self._engine.step_async(np.asarray(actions, np.float32).reshape(-1))
+            return
+        grouped, start = [], 0
+        for n in self.agent_no_list:
+            grouped.append(actions[start:start + n])
+            start += n
+        self._host.step_async(grouped)
+
+    def step_wait(self):
+        self.waiting = False
+        if self._engine is not None:
+            out = self._engine.step_wait()
+            P = self._engine.n_params
+            states = out['obs'].copy()
+            rewards = out['reward'].copy()
+            terminals = out['done'].astype(bool)
+            env_rewards, env_dones = rewards[::P], terminals[::P]
+            lengths = out['episode_len'].copy()
+            info = out['info'].copy()
+            episodes = {}
+            infos = _RowInfos(info, env_rewards, env_dones, lengths, P, episodes)
+            if self.monitor is not None:
+                episodes.update(self.monitor.step(env_rewards, env_dones, infos.per_env()))
+                for env, ep in episodes.items():
+                    infos.env_info(env)['episode'] = ep
+        else:
+            results = [remote.recv() for remote in self._host.remotes]
+            self._host.waiting = False
+            obs, rews, dones, infos = zip(*results)
+            states = np.stack([o for group in obs for o in group])
+            rewards = np.stack([r for group in rews for r in group])
+            terminals = np.stack([d for group in dones for d in group])
+            infos = [i for group in infos for i in group]
+        for callback in self.callbacks:
+            callback(states, rewards, terminals, infos)
+        return states, rewards, terminals, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def reset(self):
+        if self._engine is not None:
+            if self.monitor is not None:
+                self.monitor.reset()
+            return self._engine.reset()
+        groups = self._host._broadcast('reset', None)
+        return np.stack([o for group in groups for o in group])
+
+    def get_attr(self, attr_name, indices=None):
+        if self._engine is None:
+            return self._host.get_attr(attr_name, indices)
+        E = self._engine.num_envs
+        idx = range(E) if indices is None else ([indices] if isinstance(indices, int) else indices)
+        if attr_name == '_num_agents':
+            return [self._engine.n_params for _ in idx]
+        if attr_name == 'current_step':
+            step = self._engine.get_state()['step']
+            return [int(step[i]) for i in idx]
+        if attr_name in ('max_batches', 'max_history'):
+            return [getattr(self._engine, attr_name) for _ in idx]
+        raise AttributeError('engine-backed OptVecEnv has no per-env attribute %r' % attr_name)
+
+    def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
+        if self._engine is None:
+            return self._host.env_method(method_name, *method_args, indices=indices,
+                                         **method_kwargs)
+        monitor_methods = ('get_episode_rewards', 'get_episode_lengths', 'get_episode_times',
+                           'get_total_steps')
+        if method_name in monitor_methods and self.monitor is not None:
+            return getattr(self.monitor, method_name)(indices)
+        if method_name in ('render', 'seed'):
+            E = self._engine.num_envs
+            return [None] * (E if indices is None else len(indices))
+        raise AttributeError('engine-backed OptVecEnv has no per-env method %r' % method_name)
+
+    def render(self, *args, **kwargs):
+        return None
+
+    def close(self):
+        if self.closed:
+            return
+        self.closed = True
+        if self._engine is not None:
+            if self.monitor is not None:
+                self.monitor.close()
+            self._engine.close()
+        else:
+            self._host.close()
+

@@ -27,6 +27,18 @@
  *                  current_step (optimize.py:45-50, baseenvironment.py:18)
  *   ce_destroy     ConcurrentVecEnv.close        custom_envs/vectorize/concurrentvecenv.py:115-125
  *
+ * Multi-agent learning-rate path (MultiOptLRs-v0 under OptVecEnv):
+ *   ce_multi_create  MultiOptLRs.__init__        custom_envs/envs/multioptlrs.py:39-61
+ *                    + OptVecEnv.__init__         custom_envs/vectorize/optvecenv.py:57-68
+ *                    + OptimizeFunction.__init__  custom_envs/problems/optimize_function.py:20-61
+ *   ce_multi_reset   OptVecEnv.reset              custom_envs/vectorize/optvecenv.py:90-91
+ *                    -> MultiOptLRs.base_reset    custom_envs/envs/multioptlrs.py:66-78
+ *   ce_multi_step    OptVecEnv.step_async/wait    custom_envs/vectorize/optvecenv.py:70-88
+ *                    -> OptEnvRunner.step         custom_envs/vectorize/optvecenv.py:38-46
+ *                    -> MultiOptLRs.base_step     custom_envs/envs/multioptlrs.py:80-129
+ *   ce_multi_step_async / ce_multi_wait / ce_multi_step_many / ce_multi_host_outputs /
+ *   ce_multi_get_state / ce_multi_set_stream / ce_multi_destroy: as for Optimize-v0.
+ *
  * Conventions
  *   - Every function returns CE_OK (0) or a negative ce_status; nothing
  *     throws across the ABI.  ce_last_error() returns a thread-local message.
@@ -142,6 +154,64 @@ int ce_host_outputs(ce_engine *eng, ce_outputs *view);
 
 int ce_get_state(ce_engine *eng, const ce_state *st);
 int ce_set_state(ce_engine *eng, const ce_state *st);
+
+/* ------------------------------------------------------------------------
+ * MultiOptLRs-v0: one agent per problem parameter picks its learning rate.
+ * Rows are (env, agent) in sorted agent-name order ('parameter-0',
+ * 'parameter-1', 'parameter-10', ...), as OptVecEnv flattens them.
+ */
+typedef struct ce_multi_engine ce_multi_engine;
+
+#define CE_MULTI_MAX_PARAMS 16
+
+typedef enum ce_function {
+    /* sum of Rosenbrock 100(y - x^2)^2 + (1 - x)^2 over coordinate pairs
+       (utils_functions.py:4-6); 2 params = the reference's default problem */
+    CE_FUNC_ROSENBROCK_PAIRS = 0
+} ce_function;
+
+/* info columns, multioptlrs.py:112-127 ('loss' is NaN when not terminal) */
+typedef enum ce_multi_info {
+    CE_INFO_LOSS = 0, CE_INFO_BATCH_LOSS, CE_INFO_WEIGHTS_MEAN, CE_INFO_WEIGHTS_SUM,
+    CE_INFO_ACTIONS_MEAN, CE_INFO_ACTIONS_STD, CE_INFO_STATES_MEAN, CE_INFO_STATES_SUM,
+    CE_INFO_GRADS_MEAN, CE_INFO_GRADS_SUM, CE_INFO_LOSS_MEAN, CE_INFO_ADJUSTED_LOSS,
+    CE_INFO_ADJUSTED_GRAD, CE_INFO_GRAD_DIFF, CE_MULTI_INFO
+} ce_multi_info;
+
+typedef struct ce_multi_config {
+    int32_t abi_version;
+    int32_t device;
+    int32_t num_envs;     /* E                                               */
+    int32_t n_params;     /* P: agents per env = problem dimensions (even)   */
+    int32_t function;     /* ce_function                                     */
+    int32_t max_history;  /* H, adjusted-history length (multioptlrs.py:39)  */
+    int32_t max_batches;  /* episode length (multioptlrs.py:39, default 400) */
+    int32_t auto_reset;   /* 1: OptVecEnv auto-reset; 0: single env          */
+    float initial_points[CE_MULTI_MAX_PARAMS];
+} ce_multi_config;
+
+typedef struct ce_multi_outputs {
+    float *obs;           /* [E*P][3H] rows                                  */
+    float *reward;        /* [E*P] (replicated per agent, optvecenv.py:43)   */
+    uint8_t *done;        /* [E*P]                                           */
+    float *info;          /* [E][CE_MULTI_INFO]                              */
+    int32_t *episode_len; /* [E] info['episode']['l']                        */
+} ce_multi_outputs;
+
+int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out);
+void ce_multi_destroy(ce_multi_engine *eng);
+int ce_multi_set_stream(ce_multi_engine *eng, void *hip_stream);
+int ce_multi_reset(ce_multi_engine *eng, const ce_multi_outputs *out, uint32_t flags);
+int ce_multi_step(ce_multi_engine *eng, const float *actions /* [E*P] rows */,
+                  const ce_multi_outputs *out, uint32_t flags);
+int ce_multi_step_async(ce_multi_engine *eng, const float *actions,
+                        const ce_multi_outputs *out, uint32_t flags);
+int ce_multi_wait(ce_multi_engine *eng);
+int ce_multi_step_many(ce_multi_engine *eng, int32_t k, const float *actions,
+                       int64_t action_step_stride, const ce_multi_outputs *out);
+int ce_multi_host_outputs(ce_multi_engine *eng, ce_multi_outputs *view);
+/* theta [E][P] (problem parameters in agent order) and current_step [E] */
+int ce_multi_get_state(ce_multi_engine *eng, float *theta, int32_t *step);
 
 #ifdef __cplusplus
 }

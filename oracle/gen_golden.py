@@ -86,11 +86,54 @@ def write_rollouts(features, targets):
             os.path.join(GOLDEN, 'optimize_lr_b32_s%d.npz' % seed), **rec)
 
 
+def rollout_multi(ndims, max_batches, max_history, steps, action_seed, low=1.0, high=3.0):
+    """OptVecEnv semantics around one MultiOptLRs env: rows in sorted agent
+    order, auto-reset on done (optvecenv.py:38-46, concurrentvecenv.py:37)."""
+    from oracle.multioptlrs import MultiOptLRs, OptEnvRunner
+    env = MultiOptLRs(ndims, max_batches=max_batches, max_history=max_history)
+    runner = OptEnvRunner(env)
+    rs = np.random.RandomState(action_seed)
+    first = np.stack(runner.reset())
+    keys = ('loss', 'batch_loss', 'weights_mean', 'weights_sum', 'actions_mean', 'actions_std',
+            'states_mean', 'states_sum', 'grads_mean', 'grads_sum', 'loss_mean',
+            'adjusted_loss', 'adjusted_grad', 'grad_diff')
+    rec = {k: [] for k in ('obs', 'reward', 'done', 'info', 'ep_len', 'theta')}
+    actions = rs.uniform(low, high, (steps, ndims, 1)).astype(np.float32)
+    for t in range(steps):
+        states, rewards, dones, infos = runner.step(list(actions[t]))
+        info = infos[0]
+        rec['ep_len'].append(info['episode']['l'])
+        rec['info'].append([np.nan if info[k] is None else float(info[k]) for k in keys])
+        rec['theta'].append(env.model.params.copy())
+        if any(dones):
+            states = runner.reset()
+        rec['obs'].append(np.stack(states))
+        rec['reward'].append(rewards[0])
+        rec['done'].append(dones[0])
+    out = {k: np.array(v) for k, v in rec.items()}
+    out['actions'] = actions
+    out['reset_obs'] = first
+    return out
+
+
+def write_multi():
+    # (name, ndims, max_batches, max_history, steps, seed, action range):
+    # stable learning rates (10^-5..10^-3.5), the configs' 10^-3..10^-1
+    # (diverges: loss > 1e4 early stop), and a mix hitting max_batches
+    cases = [('multi_func2_h5', 2, 400, 5, 150, 7, -1.0, 0.5),
+             ('multi_func4_h5', 4, 400, 5, 60, 8, 1.0, 3.0),
+             ('multi_func4_h3_b25', 4, 25, 3, 90, 9, -1.0, 0.7)]
+    for name, ndims, max_batches, hist, steps, seed, low, high in cases:
+        rec = rollout_multi(ndims, max_batches, hist, steps, seed, low, high)
+        np.savez_compressed(os.path.join(GOLDEN, name + '.npz'), **rec)
+
+
 def main():
     os.makedirs(GOLDEN, exist_ok=True)
     features, targets = write_dataset()
     write_seeding(features)
     write_rollouts(features, targets)
+    write_multi()
 
 
 if __name__ == '__main__':
