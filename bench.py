@@ -1,6 +1,7 @@
 """Benchmark: vectorised Optimize-v0 env-steps/s on MI355X (BASELINE.json metric).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--precision f64|f32]
+                  [--workload optimize|multi] [--gather]
 
 One "step" = one VecEnv.step of every env: the fused HIP kernel advances
 E = 4096 envs per GPU (weak scaling: N GPUs own N*4096 envs, contiguous
@@ -10,7 +11,12 @@ one Optimize-v0 step, auto-reset included.  Actions are device-resident
 outputs (obs/reward/done/info) are written to HBM every step.  Steps are
 replayed as hipGraphs of S consecutive launches (ce_step_many).  Envs are
 independent, so there is no data-path collective; ``--gather`` adds the
-optional RCCL all-gather of the packed outputs per step (reported apart).
+north star's RCCL all-gather of the packed outputs every step (config 4,
+custom_envs_amd/distributed.py), reported as its own line.
+
+``--workload multi`` measures config 5 instead: MultiOptLRs-v0 (4 agents,
+4-D Rosenbrock pairs, H=5, max_batches=400) behind OptVecEnv, 1024 envs per
+GPU, actions uniform(1, 3) as in SURVEY 8d.
 
 Rank 0 prints ONE JSON line.  With N>1 run under
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
@@ -28,12 +34,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = 'vectorised env-steps/sec, Optimize-v0 @4096 envs, 1/2/4/8 MI355X vs host CPU'
+METRIC_MULTI = ('vectorised env-steps/sec, MultiOptLRs-v0 (4 agents) via OptVecEnv, '
+                'config 5, MI355X vs host CPU')
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 F64_VALU_PEAK_TFLOPS = 78.6
 
 
 def algorithmic_bytes_per_env_step(n_params, precision):
-    """Bytes one env-step must move given the state it carries.
+    """Bytes one Optimize env-step must move given the state it carries.
 
     action read 4P; W read+write and G read+write at sizeof(T) each; loss
     scalar (f64) read+write 16; step counter read+write 8; obs write
@@ -45,12 +53,25 @@ def algorithmic_bytes_per_env_step(n_params, precision):
     return 4 * n_params + 4 * t * n_params + 16 + 8 + 4 * (2 * n_params + 1) + 16 + 1
 
 
+def multi_bytes_per_env_step(P, H, raw=5):
+    """Bytes one MultiOptLRs env-step moves (DESIGN.md 3.6): actions 4P;
+    theta and gradient r/w 16P; raw history: newest loss/grad/weight written
+    (4 + 8P), the previous weights read (4P), all `raw` losses and gradients
+    read for the info means (raw*(4 + 4P)); adjusted history (float64): one
+    entry written (8 + 16P), H entries read for the observation (H*(8 + 16P));
+    step r/w 8; outputs: obs 4*3H*P, reward 4P, done P, info 56, length 4."""
+    return (4 * P + 16 * P + (4 + 8 * P) + 4 * P + raw * (4 + 4 * P) + (8 + 16 * P)
+            + H * (8 + 16 * P) + 8 + 12 * H * P + 4 * P + P + 56 + 4)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=2000)
     p.add_argument('--warmup', type=int, default=200)
-    p.add_argument('--envs', type=int, default=4096, help='envs per GPU')
+    p.add_argument('--envs', type=int, default=None,
+                   help='envs per GPU (default 4096 optimize, 1024 multi)')
+    p.add_argument('--workload', default='optimize', choices=['optimize', 'multi'])
     p.add_argument('--precision', default='f64', choices=['f64', 'f32'])
     p.add_argument('--graph-steps', type=int, default=250, help='steps per hipGraph replay')
     p.add_argument('--gather', action='store_true', help='all-gather outputs every step')
@@ -58,7 +79,10 @@ def parse():
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--profile-only', action='store_true',
                    help='run the timed steps only (for rocprofv3)')
-    return p.parse_args()
+    args = p.parse_args()
+    if args.envs is None:
+        args.envs = 4096 if args.workload == 'optimize' else 1024
+    return args
 
 
 def lr_dataset():
@@ -67,16 +91,33 @@ def lr_dataset():
     return seq.features, seq.targets
 
 
-def cpu_baseline(features, targets, envs, budget_s):
-    """The reference's NumPy path restated: oracle envs under ThreadVecEnv."""
-    from oracle.optimize import Optimize as OracleEnv
-    from oracle.vectorize import ThreadVecEnv
+def _raise_fd_limit(envs):
     soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
     want = 4 * envs + 256
     if soft < want and (hard == resource.RLIM_INFINITY or hard >= want):
         resource.setrlimit(resource.RLIMIT_NOFILE, (want, hard))
         soft = want
-    n = min(envs, max(1, (soft - 256) // 4))
+    return min(envs, max(1, (soft - 256) // 4))
+
+
+def _time_cpu(venv, acts, budget_s):
+    venv.step(acts)                                   # warm-up
+    steps = 0
+    wall0, cpu0 = time.perf_counter(), time.process_time()
+    while True:
+        venv.step(acts)
+        steps += 1
+        wall = time.perf_counter() - wall0
+        if wall >= budget_s or steps >= 1000:
+            break
+    return steps, wall, time.process_time() - cpu0
+
+
+def cpu_baseline(features, targets, envs, budget_s):
+    """The reference's NumPy path restated: oracle envs under ThreadVecEnv."""
+    from oracle.optimize import Optimize as OracleEnv
+    from oracle.vectorize import ThreadVecEnv
+    n = _raise_fd_limit(envs)
 
     def factory(seed):
         def make():
@@ -87,18 +128,8 @@ def cpu_baseline(features, targets, envs, budget_s):
 
     venv = ThreadVecEnv([factory(i) for i in range(n)])
     venv.reset()
-    rs = np.random.RandomState(0)
-    acts = rs.normal(0, 0.01, (n, 20)).astype(np.float32)
-    venv.step(acts)                                   # warm-up
-    steps = 0
-    wall0, cpu0 = time.perf_counter(), time.process_time()
-    while True:
-        venv.step(acts)
-        steps += 1
-        wall = time.perf_counter() - wall0
-        if wall >= budget_s or steps >= 1000:
-            break
-    cpu = time.process_time() - cpu0
+    acts = np.random.RandomState(0).normal(0, 0.01, (n, 20)).astype(np.float32)
+    steps, wall, cpu = _time_cpu(venv, acts, budget_s)
     venv.close()
     return {'value': n * steps / wall, 'unit': 'env-steps/s',
             'cores': max(1, int(round(cpu / wall))), 'kind': 'port',
@@ -106,6 +137,46 @@ def cpu_baseline(features, targets, envs, budget_s):
                       'pickled step msgs, np.stack) over the float64 numpy oracle '
                       'Optimize env; %.1f s wall, %.1f s CPU; os.cpu_count()=%d'
                       % (n, steps, wall, cpu, os.cpu_count())}
+
+
+def cpu_baseline_multi(envs, budget_s):
+    """OptVecEnv restated (ThreadVecEnv of OptEnvRunner over MultiOptLRs)."""
+    from oracle.multioptlrs import MultiOptLRs, OptVecEnv
+    n = _raise_fd_limit(envs)
+    venv = OptVecEnv([lambda: MultiOptLRs(4, max_batches=400, max_history=5)] * n)
+    venv.reset()
+    acts = np.random.RandomState(7).uniform(1, 3, (4 * n, 1)).astype(np.float32)
+    steps, wall, cpu = _time_cpu(venv, acts, budget_s)
+    venv.close()
+    return {'value': n * steps / wall, 'unit': 'env-steps/s',
+            'cores': max(1, int(round(cpu / wall))), 'kind': 'port',
+            'sample': '%d envs x 4 agents x %d steps of OptVecEnv over ThreadVecEnv '
+                      '(1 thread + mp.Pipe per env) around the numpy oracle MultiOptLRs; '
+                      '%.1f s wall, %.1f s CPU; os.cpu_count()=%d'
+                      % (n, steps, wall, cpu, os.cpu_count())}
+
+
+def build_optimize(args, torch, device, rank, world):
+    from custom_envs_amd.engine import OptimizeEngine
+    features, targets = lr_dataset()
+    E = args.envs
+    eng = OptimizeEngine(features, targets, num_envs=E, precision=args.precision,
+                         device=device)
+    eng.seed([rank * E + i for i in range(E)])
+    gen = torch.Generator(device='cuda').manual_seed(1234 + rank)
+    S = max(1, min(args.graph_steps, args.steps))
+    actions = torch.randn((S, E, eng.act_dim), generator=gen, device='cuda') * 0.01
+    return eng, actions, S
+
+
+def build_multi(args, torch, device, rank, world):
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    E = args.envs
+    eng = MultiOptEngine(E, 'func4', max_batches=400, max_history=5, device=device)
+    gen = torch.Generator(device='cuda').manual_seed(7 + rank)
+    S = max(1, min(args.graph_steps, args.steps))
+    actions = torch.rand((S, E * eng.n_params), generator=gen, device='cuda') * 2.0 + 1.0
+    return eng, actions, S
 
 
 def main():
@@ -122,45 +193,33 @@ def main():
     else:
         torch.cuda.set_device(0)
     device = torch.cuda.current_device()
+    multi = args.workload == 'multi'
 
-    from custom_envs_amd.engine import OptimizeEngine
-    features, targets = lr_dataset()
+    eng, actions, S = (build_multi if multi else build_optimize)(args, torch, device, rank,
+                                                                 world)
     E = args.envs
-    eng = OptimizeEngine(features, targets, num_envs=E, precision=args.precision,
-                         device=device)
-    P = eng.act_dim
-    eng.seed([rank * E + i for i in range(E)])
     stream = torch.cuda.Stream()          # a real stream: graphs cannot capture the null stream
     torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
-    out = eng.alloc_device_outputs()
-    S = max(1, min(args.graph_steps, args.steps))
-    gen = torch.Generator(device='cuda').manual_seed(1234 + rank)
-    actions = torch.randn((S, E, P), generator=gen, device='cuda') * 0.01
-    eng.reset_device(out)
-
-    packed = gathered = None
+    shard = None
     if args.gather and dist is not None:
-        rec = 2 * P + 1 + 5
-        packed = torch.empty((E, rec), device='cuda')
-        gathered = torch.empty((world * E, rec), device='cuda')
+        from custom_envs_amd.distributed import ShardedEnvs
+        shard = ShardedEnvs(eng, world * E, rank, world)
+        out = shard.out                   # the engine writes straight into the packed buffer
+    else:
+        out = eng.alloc_device_outputs()
+    eng.reset_device(out)
 
     def run(k):
         done = 0
         while done < k:
             n = min(S, k - done)
-            if packed is None:
+            if shard is None:
                 eng.step_many_device(n, actions, out)
             else:
                 for s in range(n):
                     eng.step_device(actions[s], out)
-                    packed[:, :2 * P + 1] = out['obs']
-                    packed[:, 2 * P + 1] = out['reward']
-                    packed[:, 2 * P + 2] = out['done']
-                    packed[:, 2 * P + 3] = out['objective']
-                    packed[:, 2 * P + 4] = out['accuracy']
-                    packed[:, 2 * P + 5] = out['episode_len']
-                    dist.all_gather_into_tensor(gathered, packed)
+                    shard.gather()
             done += n
 
     run(args.warmup)
@@ -195,86 +254,144 @@ def main():
         eng.step_device(actions[i % S], out)
         ends[i].record(stream)
     torch.cuda.synchronize()
-    kernel_ms = float(np.median([s.elapsed_time(e) for s, e in zip(starts, ends)]))
-    kernel_ms_mean = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    times = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    kernel_ms, kernel_ms_mean = float(np.median(times)), float(np.mean(times))
 
-    # host-loop rate (numpy actions in, numpy outputs out: PCIe-inclusive)
     host_rate = None
-    if rank == 0 and world == 1:
-        heng = OptimizeEngine(features, targets, num_envs=E, precision=args.precision,
-                              device=device)
-        heng.seed(list(range(E)))
-        heng.reset()
-        hact = np.random.RandomState(5).normal(0, 0.01, (E, P)).astype(np.float32)
-        for _ in range(20):
-            heng.step(hact)
-        h0 = time.perf_counter()
-        hn = 300
-        for _ in range(hn):
-            o = heng.step(hact)
-            o['obs'].copy()
-        host_rate = E * hn / (time.perf_counter() - h0)
-        heng.close()
-
+    if rank == 0 and world == 1 and not multi:
+        host_rate = host_loop_rate(args, device, E)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(features, targets, E, args.cpu_seconds)
+        cpu = (cpu_baseline_multi(E, args.cpu_seconds) if multi else
+               cpu_baseline(*lr_dataset(), E, args.cpu_seconds))
 
     if rank == 0:
-        env_steps = world * E * args.steps
-        bpe = algorithmic_bytes_per_env_step(P, args.precision)
-        achieved_gbs = bpe * E / (kernel_ms * 1e-3) / 1e9
-        traffic = None
-        pmc_path = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
-        if os.path.exists(pmc_path):
-            with open(pmc_path) as fh:
-                pmc = json.load(fh)
-            if pmc.get('envs') == E and pmc.get('precision') == args.precision:
-                traffic = pmc.get('hbm_bytes_per_launch')
-        line = {
-            'metric': METRIC,
-            'value': env_steps / elapsed,
-            'unit': 'env-steps/s',
-            'n_gpus': world,
-            'steps': args.steps,
-            'warmup': args.warmup,
-            'ms_per_step': elapsed / args.steps * 1e3,
-            'higher_is_better': True,
-            'scaling': 'weak',
-            'vs_baseline': None,
-            'dtype': args.precision,
-            'data': 'synthetic: make_classification(256 x 10, random_state=0) one-hot(2); '
-                    'actions N(0, 0.01) float32 generated on device',
-            'config': {
-                'workload': 'Optimize-v0 softmax-regression 256x10 (P=20, obs 41), '
-                            '%d envs per GPU, B=N=256, 40-step episodes with in-kernel '
-                            'auto-reset, device-resident actions/outputs' % E,
-                'envs_per_gpu': E, 'global_envs': world * E, 'n_rows': 256,
-                'n_features': 10, 'n_classes': 2, 'batch_size': 256,
-                'graph_steps': S, 'parallelism': 'env-sharded x%d (no collective)' % world
-                if packed is None else 'env-sharded x%d + all-gather/step' % world,
-            },
-            'roofline': {
-                'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
-                'traffic': traffic,
-                'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
-                'kernel_ms_mean': kernel_ms_mean,
-                'kernel': 'ce::optimize_step_kernel<%s,10,2>' % (
-                    'double' if args.precision == 'f64' else 'float'),
-                # the limiter is the f64/f32 VALU, not HBM:
-                # algorithmic FLOPs 2NFK (logits) + 2NFK (X^T(P-Y)) + 5NK
-                'flops_per_env_step': 4 * 256 * P + 5 * 256 * 2,
-                'valu_tflops': (4 * 256 * P + 5 * 256 * 2) * E / (kernel_ms * 1e-3) / 1e12,
-                'valu_peak_tflops': F64_VALU_PEAK_TFLOPS if args.precision == 'f64' else 157.3,
-            },
-            'cpu_baseline': cpu,
-            'host_loop_env_steps_per_s': host_rate,
-        }
+        line = (multi_line if multi else optimize_line)(args, eng, world, E, S, elapsed,
+                                                        kernel_ms, kernel_ms_mean, shard)
+        line['cpu_baseline'] = cpu
+        if host_rate is not None:
+            line['host_loop_env_steps_per_s'] = host_rate
         print(json.dumps(line))
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def host_loop_rate(args, device, E):
+    """numpy actions in, numpy outputs out: the PCIe-inclusive VecEnv rate."""
+    from custom_envs_amd.engine import OptimizeEngine
+    features, targets = lr_dataset()
+    heng = OptimizeEngine(features, targets, num_envs=E, precision=args.precision,
+                          device=device)
+    heng.seed(list(range(E)))
+    heng.reset()
+    hact = np.random.RandomState(5).normal(0, 0.01, (E, heng.act_dim)).astype(np.float32)
+    for _ in range(20):
+        heng.step(hact)
+    h0 = time.perf_counter()
+    hn = 300
+    for _ in range(hn):
+        o = heng.step(hact)
+        o['obs'].copy()
+    rate = E * hn / (time.perf_counter() - h0)
+    heng.close()
+    return rate
+
+
+def _common(args, world, E, S, elapsed, shard):
+    return {
+        'value': world * E * args.steps / elapsed,
+        'unit': 'env-steps/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': elapsed / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+    }
+
+
+def _pmc_traffic(E, precision, kernel):
+    pmc_path = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
+    if not os.path.exists(pmc_path):
+        return None
+    with open(pmc_path) as fh:
+        pmc = json.load(fh)
+    entry = pmc.get(kernel) if isinstance(pmc.get(kernel), dict) else (
+        pmc if kernel == 'optimize' else {})
+    if entry.get('envs') == E and entry.get('precision') == precision:
+        return entry.get('hbm_bytes_per_launch')
+    return None
+
+
+def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
+    P = eng.act_dim
+    bpe = algorithmic_bytes_per_env_step(P, args.precision)
+    achieved_gbs = bpe * E / (kernel_ms * 1e-3) / 1e9
+    flops = 4 * 256 * P + 5 * 256 * 2
+    line = {'metric': METRIC}
+    line.update(_common(args, world, E, S, elapsed, shard))
+    line.update({
+        'dtype': args.precision,
+        'data': 'synthetic: make_classification(256 x 10, random_state=0) one-hot(2); '
+                'actions N(0, 0.01) float32 generated on device',
+        'config': {
+            'workload': 'Optimize-v0 softmax-regression 256x10 (P=20, obs 41), '
+                        '%d envs per GPU, B=N=256, 40-step episodes with in-kernel '
+                        'auto-reset, device-resident actions/outputs' % E,
+            'envs_per_gpu': E, 'global_envs': world * E, 'n_rows': 256,
+            'n_features': 10, 'n_classes': 2, 'batch_size': 256,
+            'graph_steps': S, 'parallelism': 'env-sharded x%d (no collective)' % world
+            if shard is None else 'env-sharded x%d + all-gather/step' % world,
+        },
+        'roofline': {
+            'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
+            'traffic': _pmc_traffic(E, args.precision, 'optimize'),
+            'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
+            'kernel_ms_mean': kernel_ms_mean,
+            'kernel': 'ce::optimize_step_kernel<%s,10,2>' % (
+                'double' if args.precision == 'f64' else 'float'),
+            # the limiter is the f64/f32 VALU, not HBM (DESIGN.md 3.4):
+            # algorithmic FLOPs 2NFK (logits) + 2NFK (X^T(P-Y)) + 5NK
+            'flops_per_env_step': flops,
+            'valu_tflops': flops * E / (kernel_ms * 1e-3) / 1e12,
+            'valu_peak_tflops': F64_VALU_PEAK_TFLOPS if args.precision == 'f64' else 157.3,
+        },
+    })
+    return line
+
+
+def multi_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
+    P, H = eng.n_params, eng.max_history
+    bpe = multi_bytes_per_env_step(P, H)
+    achieved_gbs = bpe * E / (kernel_ms * 1e-3) / 1e9
+    line = {'metric': METRIC_MULTI}
+    line.update(_common(args, world, E, S, elapsed, shard))
+    line.update({
+        'agent_steps_per_s': P * world * E * args.steps / elapsed,
+        'dtype': 'f32',
+        'data': 'synthetic: 4-D Rosenbrock pairs from [-1.9, 2, -1.9, 2]; actions '
+                'uniform(1, 3) float32 generated on device (lr 1e-3..1e-1)',
+        'config': {
+            'workload': 'MultiOptLRs-v0 x OptVecEnv, P=4 agents, H=5, max_batches=400, '
+                        '%d envs (%d agent rows) per GPU, in-kernel auto-reset, '
+                        'device-resident actions/outputs' % (E, E * P),
+            'envs_per_gpu': E, 'global_envs': world * E, 'agents': P, 'max_history': H,
+            'graph_steps': S, 'parallelism': 'env-sharded x%d (no collective)' % world
+            if shard is None else 'env-sharded x%d + all-gather/step' % world,
+        },
+        'roofline': {
+            'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
+            'traffic': _pmc_traffic(E, 'f32', 'multi'),
+            'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
+            'kernel_ms_mean': kernel_ms_mean,
+            'kernel': 'ce::multi_step_kernel<4>',
+        },
+    })
+    return line
 
 
 if __name__ == '__main__':

@@ -222,4 +222,39 @@ void reset_draws(uint64_t seed, int n_features, int n_classes, int n_rows,
     }
 }
 
+static void legacy_shuffle(Mt19937 &rng, int n_rows, int32_t *perm) {
+    for (int i = 0; i < n_rows; ++i) perm[i] = i;
+    for (int i = n_rows - 1; i > 0; --i) {
+        const int j = static_cast<int>(rng.interval(static_cast<uint64_t>(i)));
+        const int32_t t = perm[i];
+        perm[i] = perm[j];
+        perm[j] = t;
+    }
+}
+
+void reset_draws_mlp(uint64_t seed, int n_features, int n_hidden, int n_classes, int n_rows,
+                     float *init_weights, int32_t *perm) {
+    uint32_t key[2];
+    const int key_len = seed_key(seed, key);
+    Mt19937 rng;
+    rng.init_by_array(key, key_len);
+    // RandomState.uniform(low, high): low + (high - low) * random_sample()
+    auto draw = [&](int fan_in, int fan_out, float *out, int count) {
+        const double limit = std::sqrt(6.0 / static_cast<double>(fan_in + fan_out));
+        const double low = -limit, range = limit - low;
+        for (int i = 0; i < count; ++i) {
+            const double v = low + range * rng.next_double();
+            if (out) out[i] = static_cast<float>(v);
+        }
+    };
+    const int w1 = n_features * n_hidden, w2 = n_hidden * n_classes;
+    draw(n_features, n_hidden, init_weights, w1);
+    draw(n_hidden, n_classes, init_weights ? init_weights + w1 + n_hidden : nullptr, w2);
+    if (init_weights) {
+        for (int i = 0; i < n_hidden; ++i) init_weights[w1 + i] = 0.0f;
+        for (int i = 0; i < n_classes; ++i) init_weights[w1 + n_hidden + w2 + i] = 0.0f;
+    }
+    if (perm) legacy_shuffle(rng, n_rows, perm);
+}
+
 }  // namespace ce

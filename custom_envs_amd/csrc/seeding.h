@@ -29,4 +29,11 @@ int seed_key(uint64_t seed, uint32_t key[2]);
 void reset_draws(uint64_t seed, int n_features, int n_classes, int n_rows,
                  double *init_weights, int32_t *perm);
 
+// (W0, perm) of the MLP problem: glorot-uniform W1
+// (F x H) then W2 (H x K) as legacy uniform(-l, l) draws rounded to float32,
+// zero biases, in the flat order [W1 | b1 | W2 | b2]; then the legacy
+// shuffle of arange(n_rows).  Either output may be null.
+void reset_draws_mlp(uint64_t seed, int n_features, int n_hidden, int n_classes, int n_rows,
+                     float *init_weights, int32_t *perm);
+
 }  // namespace ce

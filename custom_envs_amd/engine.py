@@ -134,16 +134,21 @@ class OptimizeEngine:
                          accuracy=out['accuracy'].data_ptr(),
                          episode_len=out['episode_len'].data_ptr())
 
+    def output_fields(self):
+        """(name, torch dtype, rows per env, trailing shape) of the step outputs."""
+        import torch
+        return [('obs', torch.float32, 1, (self.obs_dim,)),
+                ('reward', torch.float32, 1, ()),
+                ('done', torch.uint8, 1, ()),
+                ('objective', torch.float32, 1, ()),
+                ('accuracy', torch.float32, 1, ()),
+                ('episode_len', torch.int32, 1, ())]
+
     def alloc_device_outputs(self, torch_device=None):
         import torch
         dev = torch_device or torch.device('cuda', self.device)
-        E = self.num_envs
-        return {'obs': torch.empty((E, self.obs_dim), dtype=torch.float32, device=dev),
-                'reward': torch.empty(E, dtype=torch.float32, device=dev),
-                'done': torch.empty(E, dtype=torch.uint8, device=dev),
-                'objective': torch.empty(E, dtype=torch.float32, device=dev),
-                'accuracy': torch.empty(E, dtype=torch.float32, device=dev),
-                'episode_len': torch.empty(E, dtype=torch.int32, device=dev)}
+        return {name: torch.empty((self.num_envs * rows,) + tail, dtype=dtype, device=dev)
+                for name, dtype, rows, tail in self.output_fields()}
 
     def _check_device_tensors(self, actions, out, steps=1):
         if actions.dtype.itemsize != 4 or not actions.is_contiguous():

@@ -85,6 +85,12 @@ class MultiOptEngine:
             'episode_len': _view(view.episode_len, E, ctypes.c_int32, np.int32, (E,)),
         }
 
+    def seed(self, seeds=None):
+        """MultiOptLRs draws nothing at reset (fixed initial_points): seeds are
+        accepted for the VecEnv surface and ignored, like the reference's
+        unused RNG (multioptlrs.py:39-48)."""
+        return seeds
+
     @property
     def rows(self):
         return self.num_envs * self.n_params
@@ -113,16 +119,21 @@ class MultiOptEngine:
         check(self._lib.ce_multi_set_stream(self._h, ctypes.c_void_p(stream_handle or 0)),
               'ce_multi_set_stream')
 
+    def output_fields(self):
+        """(name, torch dtype, rows per env, trailing shape) of the step outputs."""
+        import torch
+        P, W = self.n_params, 3 * self.max_history
+        return [('obs', torch.float32, P, (W,)),
+                ('reward', torch.float32, P, ()),
+                ('done', torch.uint8, P, ()),
+                ('info', torch.float32, 1, (len(_native.MULTI_INFO_KEYS),)),
+                ('episode_len', torch.int32, 1, ())]
+
     def alloc_device_outputs(self, torch_device=None):
         import torch
         dev = torch_device or torch.device('cuda')
-        E, P, W = self.num_envs, self.n_params, 3 * self.max_history
-        return {'obs': torch.empty((E * P, W), dtype=torch.float32, device=dev),
-                'reward': torch.empty(E * P, dtype=torch.float32, device=dev),
-                'done': torch.empty(E * P, dtype=torch.uint8, device=dev),
-                'info': torch.empty((E, len(_native.MULTI_INFO_KEYS)), dtype=torch.float32,
-                                    device=dev),
-                'episode_len': torch.empty(E, dtype=torch.int32, device=dev)}
+        return {name: torch.empty((self.num_envs * rows,) + tail, dtype=dtype, device=dev)
+                for name, dtype, rows, tail in self.output_fields()}
 
     @staticmethod
     def _outputs(out):

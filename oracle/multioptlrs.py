@@ -11,11 +11,12 @@ Follows, line by line:
   custom_envs/vectorize/optvecenv.py:10-91    (flatten_dictionary,
                                                OptEnvRunner, OptVecEnv)
 
-The TF1 problem is restated in float32 numpy with the analytic Rosenbrock
-gradient (TF's own op order is not reproducible here: parity of the float32
-problem values is "unpinned" beyond float32 rounding).  Build-defined (SURVEY
-8d config 5): ``rosenbrock_pairs`` = sum of Rosenbrock over consecutive
-coordinate pairs, start [-1.9, 2.0] repeated.
+The TF1 problem is restated in float32 numpy in the order TF1's graph and
+tf.gradients evaluate it (RosenbrockPairs._eval).  TF itself is absent, so
+that order is read off the graph, not run: parity of the float32 problem
+values against TF is "unpinned" beyond float32 rounding.  Build-defined
+(SURVEY 8d config 5): ``rosenbrock_pairs`` = sum of Rosenbrock over
+consecutive coordinate pairs, start [-1.9, 2.0] repeated.
 """
 from collections import deque
 from itertools import chain, cycle
@@ -236,3 +237,40 @@ class OptEnvRunner:
         states, reward, terminal, info = self._environment.step(actions)
         n = self._num_agents
         return flatten_dictionary(states), [reward] * n, [terminal] * n, [info] * n
+
+    def __getattr__(self, attr):                          # optvecenv.py:51-54
+        if attr.startswith('_'):
+            raise AttributeError(attr)
+        return getattr(self._environment, attr)
+
+
+class OptVecEnv:
+    """optvecenv.py:57-91 over the restated ThreadVecEnv (the reference's
+    multi-agent vector path; bench.py's config-5 CPU baseline)."""
+
+    def __init__(self, environment_fns):
+        from oracle.vectorize import ThreadVecEnv
+        self.venv = ThreadVecEnv([_runner_factory(fn) for fn in environment_fns])
+        self.agent_no_list = self.venv.get_attr('_num_agents')
+        self.num_envs = sum(self.agent_no_list)
+
+    def reset(self):
+        return np.concatenate(list(self.venv.reset()))
+
+    def step(self, actions):
+        grouped, start = [], 0
+        for n in self.agent_no_list:                       # optvecenv.py:70-76
+            grouped.append(list(actions[start:start + n]))
+            start += n
+        states, rewards, dones, infos = self.venv.step(grouped)
+        return (np.concatenate(list(states)), np.concatenate(list(rewards)),
+                np.concatenate(list(dones)), [i for group in infos for i in group])
+
+    def close(self):
+        self.venv.close()
+
+
+def _runner_factory(fn):
+    def make():
+        return OptEnvRunner(fn())
+    return make

@@ -19,6 +19,17 @@ Build-defined pieces (the reference does not ship them):
       accuracy ``mean(argmax P == argmax Y)``.
   A9  ``sequence.shuffle`` == ``on_epoch_end``; ``label_shape`` ==
       ``target_shape``; ``labels`` == ``targets``.
+  A12 ``model='mlp'`` (config 3): the Optimize env over a float32 MLP
+      F -> hidden (relu) -> K (softmax), the OptimizeNN network
+      (problems/optimize_nn.py:35-52, utils_tf.py:74-86) in numpy.  Flat
+      parameters in Keras ``trainable_variables`` order [W1 (F,H) row-major,
+      b1, W2 (H,K), b2] (utils_common.flatten_arrays); ``reset`` draws
+      glorot-uniform W1 then W2 from the global RandomState
+      (``uniform(-l, l)``, l = sqrt(6 / (fan_in + fan_out)), cast to
+      float32), zero biases; ``compute_backprop`` returns the float32 mean
+      cross-entropy (the ModelNumpy form ``-log(P + 1e-16)``), the summed
+      gradient (tf.gradients of the per-sample loss vector, optimize_nn.py:
+      48-52) and the accuracy.  The env's histories stay float64 (np.zeros).
 
 The oracle also records ``order``: the dataset-row index of every current
 row, composed exactly as ``on_epoch_end`` composes permutations, so tests can
@@ -126,20 +137,71 @@ class ModelNumpy:
         return loss, grad, accuracy
 
 
+class ModelMLP:
+    """A12: float32 F -> hidden (relu) -> K (softmax) classifier, flat params."""
+
+    def __init__(self, feature_size, num_of_labels, hidden=64):
+        F, H, K = feature_size, hidden, num_of_labels
+        self.dims = (F, H, K)
+        self.shapes = ((F, H), (H,), (H, K), (K,))
+        self.size = F * H + H + H * K + K
+        self.weights = np.zeros(self.size, np.float32)
+
+    def reset(self):
+        F, H, K = self.dims
+        w1 = npr.uniform(-np.sqrt(6.0 / (F + H)), np.sqrt(6.0 / (F + H)), (F, H))
+        w2 = npr.uniform(-np.sqrt(6.0 / (H + K)), np.sqrt(6.0 / (H + K)), (H, K))
+        self.weights = np.concatenate([w1.ravel(), np.zeros(H), w2.ravel(),
+                                       np.zeros(K)]).astype(np.float32)
+
+    def set_weights(self, weights):
+        self.weights = np.asarray(weights, np.float32).reshape(-1)
+
+    def unflatten(self):
+        out, start = [], 0
+        for shape in self.shapes:
+            n = int(np.prod(shape))
+            out.append(self.weights[start:start + n].reshape(shape))
+            start += n
+        return out
+
+    def compute_backprop(self, features, labels):
+        w1, b1, w2, b2 = self.unflatten()
+        z1 = features @ w1 + b1
+        hid = np.maximum(z1, np.float32(0))
+        prob = softmax(hid @ w2 + b2)
+        loss = cross_entropy(prob, labels)
+        dz2 = prob - labels
+        dz1 = (dz2 @ w2.T) * (z1 > 0)
+        grad = np.concatenate([(features.T @ dz1).ravel(), dz1.sum(axis=0),
+                               (hid.T @ dz2).ravel(), dz2.sum(axis=0)])
+        accuracy = np.mean(np.argmax(prob, axis=1) == np.argmax(labels, axis=1))
+        return loss, grad, accuracy
+
+
 class Optimize:
     """optimize.py:14-109 over baseenvironment.py:11-57."""
 
-    def __init__(self, features, targets, batch_size=None, max_steps=40):
+    def __init__(self, features, targets, batch_size=None, max_steps=40, model='linear',
+                 hidden=64):
         # BaseEnvironment.__init__ (:16-18)
         self.random_generator, _ = np_random()
         self.current_step = 0
         # Optimize.__init__ (:40-56); load_data replaced by explicit arrays
+        if model == 'mlp':              # the TF feed is float32 (optimize_nn.py:35-36)
+            features = np.asarray(features, np.float32)
+            targets = np.asarray(targets, np.float32)
         self.sequence = InMemoryDataSet(features, targets, batch_size)
         num_of_labels = self.sequence.label_shape[0]
         feature_size = self.sequence.feature_shape[0]
-        self.model = ModelNumpy(feature_size, num_of_labels)
+        if model == 'mlp':
+            self.model = ModelMLP(feature_size, num_of_labels, hidden)
+            hist_shape = (3, self.model.size)
+        else:
+            self.model = ModelNumpy(feature_size, num_of_labels)
+            hist_shape = (3, feature_size, num_of_labels)
         self.loss_hist = np.zeros((3, 1))
-        self.grad_hist = np.zeros((3, feature_size, num_of_labels))
+        self.grad_hist = np.zeros(hist_shape)
         self.wght_hist = np.zeros(self.grad_hist.shape)
         self.obs_size = 2 * self.model.size + 1
         self.max_steps = max_steps
@@ -204,6 +266,19 @@ class Optimize:
 
     def close(self):
         pass
+
+
+def initial_draws_mlp(seed, n_features, hidden, n_classes, n_rows):
+    """(W0 flat float32, perm) of the A12 MLP: uniform W1, uniform W2, then
+    shuffle(arange(N)), all from the env's (never advanced) RandomState."""
+    rng, _ = np_random(seed)
+    F, H, K = n_features, hidden, n_classes
+    w1 = rng.uniform(-np.sqrt(6.0 / (F + H)), np.sqrt(6.0 / (F + H)), (F, H))
+    w2 = rng.uniform(-np.sqrt(6.0 / (H + K)), np.sqrt(6.0 / (H + K)), (H, K))
+    weights = np.concatenate([w1.ravel(), np.zeros(H), w2.ravel(), np.zeros(K)])
+    perm = np.arange(n_rows)
+    rng.shuffle(perm)
+    return weights.astype(np.float32), perm
 
 
 def initial_draws(seed, n_features, n_classes, n_rows):
