@@ -12,9 +12,9 @@ LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd.so')
 if os.environ.get('CE_LIB') == 'diag':
     LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd_diag.so')
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 CE_OK, CE_EINVAL, CE_EHIP, CE_ENOMEM, CE_ESTATE, CE_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
-CE_PROBLEM_SOFTMAX = 0
+CE_PROBLEM_SOFTMAX, CE_PROBLEM_MLP = 0, 1
 CE_F64, CE_F32 = 0, 1
 CE_PTR_DEVICE = 1
 
@@ -24,7 +24,8 @@ STATUS_NAMES = {CE_EINVAL: 'CE_EINVAL', CE_EHIP: 'CE_EHIP', CE_ENOMEM: 'CE_ENOME
 # Every symbol include/custom_envs_amd.h declares.
 EXPORTS = (
     'ce_abi_version', 'ce_last_error', 'ce_create', 'ce_destroy', 'ce_set_stream',
-    'ce_num_envs', 'ce_obs_dim', 'ce_act_dim', 'ce_seed', 'ce_seed_draws', 'ce_reset',
+    'ce_num_envs', 'ce_obs_dim', 'ce_act_dim', 'ce_seed', 'ce_seed_draws',
+    'ce_seed_draws_mlp', 'ce_reset',
     'ce_step', 'ce_step_async', 'ce_wait', 'ce_step_many', 'ce_host_outputs',
     'ce_get_state', 'ce_set_state',
     'ce_multi_create', 'ce_multi_destroy', 'ce_multi_set_stream', 'ce_multi_reset',
@@ -46,7 +47,7 @@ class NativeEngineError(RuntimeError):
 class CeConfig(ctypes.Structure):
     _fields_ = [(name, ctypes.c_int32) for name in (
         'abi_version', 'problem', 'precision', 'device', 'num_envs', 'n_rows',
-        'n_features', 'n_classes', 'batch_size', 'max_steps', 'auto_reset')]
+        'n_features', 'n_classes', 'batch_size', 'max_steps', 'auto_reset', 'n_hidden')]
 
 
 class CeOutputs(ctypes.Structure):
@@ -89,6 +90,7 @@ def _declare(lib):
         'ce_act_dim': ([vp], ctypes.c_int),
         'ce_seed': ([vp, vp, i32], ctypes.c_int),
         'ce_seed_draws': ([ctypes.c_uint64, i32, i32, i32, vp, vp], ctypes.c_int),
+        'ce_seed_draws_mlp': ([ctypes.c_uint64, i32, i32, i32, i32, vp, vp], ctypes.c_int),
         'ce_reset': ([vp, ctypes.POINTER(CeOutputs), u32], ctypes.c_int),
         'ce_step': ([vp, vp, ctypes.POINTER(CeOutputs), u32], ctypes.c_int),
         'ce_step_async': ([vp, vp, ctypes.POINTER(CeOutputs), u32], ctypes.c_int),

@@ -17,7 +17,11 @@
 #include <string>
 #include <vector>
 
+#include <algorithm>
+#include <thread>
+
 #include "common.h"
+#include "mlp_kernels.h"
 #include "optimize_kernels.h"
 #include "seeding.h"
 
@@ -69,7 +73,9 @@ const KernelEntry *find_kernel(int precision, int F, int K) {
 struct ce_engine {
     ce_config cfg{};
     int P = 0, obs_dim = 0;
-    size_t tsize = 8;  // sizeof(T)
+    bool mlp = false;  // CE_PROBLEM_MLP
+    size_t tsize = 8;  // element size of W / W0
+    size_t gsize = 8;  // element size of G (grad_hist)
     const KernelEntry *kern = nullptr;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -145,8 +151,48 @@ int grid_of(const ce_engine *e) {
     return (e->cfg.num_envs + ce::kWavesPerBlock - 1) / ce::kWavesPerBlock;
 }
 
+ce::MlpArgs make_mlp_args(const ce_engine *e, const float *act, const ce_outputs &o) {
+    ce::MlpArgs a;
+    a.E = e->cfg.num_envs;
+    a.N = e->cfg.n_rows;
+    a.F = e->cfg.n_features;
+    a.K = e->cfg.n_classes;
+    a.P = e->P;
+    a.max_steps = e->cfg.max_steps;
+    a.auto_reset = e->cfg.auto_reset;
+    a.X = static_cast<const float *>(e->X);
+    a.label = e->label;
+    a.W = static_cast<float *>(e->W);
+    a.W0 = static_cast<const float *>(e->W0);
+    a.G = static_cast<double *>(e->G);
+    a.L = e->L;
+    a.step = e->step;
+    a.perm = e->perm;
+    a.order = e->order;
+    a.order_sel = e->order_sel;
+    a.act = act;
+    a.obs = o.obs;
+    a.reward = o.reward;
+    a.done = o.done;
+    a.objective = o.objective;
+    a.accuracy = o.accuracy;
+    a.episode_len = o.episode_len;
+    return a;
+}
+
 void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &o,
             hipStream_t stream) {
+    if (e->mlp) {
+        const ce::MlpArgs a = make_mlp_args(e, act, o);
+        const dim3 grid(e->cfg.num_envs), block(ce::kMlpBlock);
+        if (reset) {
+            hipLaunchKernelGGL(ce::mlp_reset_kernel, grid, block, 0, stream, a);
+        } else {
+            hipLaunchKernelGGL(ce::mlp_train_kernel, grid, block, 0, stream, a);
+            hipLaunchKernelGGL(ce::mlp_info_kernel, grid, block, 0, stream, a);
+        }
+        return;
+    }
     StepFn fn = reset ? e->kern->reset : (e->staged ? e->kern->step_staged : e->kern->step_global);
     if (e->cfg.precision == CE_F64) {
         auto a = make_args<double>(e, act, o);
@@ -157,9 +203,9 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
     }
 }
 
-// Convert host float64 rows to the engine's compute type and upload.
-int upload_typed(ce_engine *e, void *dst, const double *src, size_t count) {
-    if (e->cfg.precision == CE_F64) {
+// Convert host float64 values to a device array of `elem`-byte floats.
+int upload_typed(ce_engine *e, void *dst, const double *src, size_t count, size_t elem) {
+    if (elem == sizeof(double)) {
         CE_HIP(hipMemcpyAsync(dst, src, count * sizeof(double), hipMemcpyHostToDevice, e->stream));
     } else {
         std::vector<float> tmp(count);
@@ -171,8 +217,8 @@ int upload_typed(ce_engine *e, void *dst, const double *src, size_t count) {
     return CE_OK;
 }
 
-int download_typed(ce_engine *e, double *dst, const void *src, size_t count) {
-    if (e->cfg.precision == CE_F64) {
+int download_typed(ce_engine *e, double *dst, const void *src, size_t count, size_t elem) {
+    if (elem == sizeof(double)) {
         CE_HIP(hipMemcpyAsync(dst, src, count * sizeof(double), hipMemcpyDeviceToHost, e->stream));
         CE_HIP(hipStreamSynchronize(e->stream));
     } else {
@@ -243,13 +289,21 @@ int ce_seed_draws(uint64_t seed, int32_t n_features, int32_t n_classes, int32_t 
     return CE_OK;
 }
 
+int ce_seed_draws_mlp(uint64_t seed, int32_t n_features, int32_t n_hidden, int32_t n_classes,
+                      int32_t n_rows, float *init_weights, int32_t *perm) {
+    if (n_features <= 0 || n_hidden <= 0 || n_classes <= 0 || n_rows < 0)
+        return fail(CE_EINVAL, "ce_seed_draws_mlp: bad shape");
+    ce::reset_draws_mlp(seed, n_features, n_hidden, n_classes, n_rows, init_weights, perm);
+    return CE_OK;
+}
+
 int ce_create(const ce_config *cfg, const double *features, const int32_t *labels,
               ce_engine **out) {
     if (!cfg || !features || !labels || !out) return fail(CE_EINVAL, "ce_create: null argument");
     *out = nullptr;
     if (cfg->abi_version != CE_ABI_VERSION)
         return fail(CE_EINVAL, "ce_create: ABI version mismatch");
-    if (cfg->problem != CE_PROBLEM_SOFTMAX)
+    if (cfg->problem != CE_PROBLEM_SOFTMAX && cfg->problem != CE_PROBLEM_MLP)
         return fail(CE_EUNSUPPORTED, "ce_create: unknown problem");
     if (cfg->precision != CE_F64 && cfg->precision != CE_F32)
         return fail(CE_EINVAL, "ce_create: unknown precision");
@@ -258,11 +312,25 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     if (cfg->batch_size <= 0 || cfg->batch_size > cfg->n_rows)
         return fail(CE_EINVAL, "ce_create: batch_size must be in [1, n_rows]");
     if (cfg->max_steps <= 0) return fail(CE_EINVAL, "ce_create: max_steps must be positive");
-    const KernelEntry *kern = find_kernel(cfg->precision, cfg->n_features, cfg->n_classes);
-    if (!kern)
-        return fail(CE_EUNSUPPORTED, "ce_create: no compiled kernel for F=" +
-                                         std::to_string(cfg->n_features) +
-                                         " K=" + std::to_string(cfg->n_classes));
+    const bool mlp = cfg->problem == CE_PROBLEM_MLP;
+    const KernelEntry *kern = nullptr;
+    if (mlp) {
+        // the shapes mlp_kernels.h is written for (config 3: 784 -> 64 -> 10, B = 32)
+        if (cfg->precision != CE_F32)
+            return fail(CE_EUNSUPPORTED, "ce_create: the MLP problem computes in float32");
+        if (cfg->n_hidden != ce::kMlpHidden || cfg->batch_size != ce::kMlpBatch ||
+            cfg->n_features % 8 != 0 || cfg->n_classes > ce::kMlpMaxK || cfg->n_rows % 64 != 0 ||
+            cfg->batch_size >= cfg->n_rows)
+            return fail(CE_EUNSUPPORTED, "ce_create: MLP needs n_hidden=64, batch_size=32 < "
+                                         "n_rows, n_rows % 64 == 0, n_features % 8 == 0, "
+                                         "n_classes <= 16");
+    } else {
+        kern = find_kernel(cfg->precision, cfg->n_features, cfg->n_classes);
+        if (!kern)
+            return fail(CE_EUNSUPPORTED, "ce_create: no compiled kernel for F=" +
+                                             std::to_string(cfg->n_features) +
+                                             " K=" + std::to_string(cfg->n_classes));
+    }
     for (int i = 0; i < cfg->n_rows; ++i)
         if (labels[i] < 0 || labels[i] >= cfg->n_classes)
             return fail(CE_EINVAL, "ce_create: label out of range");
@@ -271,9 +339,18 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     if (!e) return fail(CE_ENOMEM, "ce_create: host allocation failed");
     e->cfg = *cfg;
     e->kern = kern;
-    e->P = cfg->n_features * cfg->n_classes;
+    e->mlp = mlp;
+    if (mlp) {
+        const int F = cfg->n_features, H = cfg->n_hidden, K = cfg->n_classes;
+        e->P = F * H + H + H * K + K;
+        e->tsize = sizeof(float);
+        e->gsize = sizeof(double);
+    } else {
+        e->P = cfg->n_features * cfg->n_classes;
+        e->tsize = cfg->precision == CE_F64 ? sizeof(double) : sizeof(float);
+        e->gsize = e->tsize;
+    }
     e->obs_dim = 2 * e->P + 1;
-    e->tsize = cfg->precision == CE_F64 ? sizeof(double) : sizeof(float);
     auto bail = [&](int code) {
         ce_destroy(e);
         return code;
@@ -291,9 +368,15 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     e->stream = e->own_stream;
 
     const size_t E = cfg->num_envs, N = cfg->n_rows, F = cfg->n_features, P = e->P;
-    CE_TRY(hipMalloc(&e->X, ce::stage_bytes_total(cfg->n_features, cfg->n_rows, static_cast<int>(e->tsize))));
+    if (mlp) {
+        CE_TRY(hipMalloc(&e->X, N * F * sizeof(float)));
+        CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
+    } else {
+        CE_TRY(hipMalloc(&e->X, ce::stage_bytes_total(cfg->n_features, cfg->n_rows,
+                                                      static_cast<int>(e->tsize))));
+    }
     CE_TRY(hipMalloc(&e->W, E * P * e->tsize));
-    CE_TRY(hipMalloc(&e->G, E * P * e->tsize));
+    CE_TRY(hipMalloc(&e->G, E * P * e->gsize));
     CE_TRY(hipMalloc(&e->W0, E * P * e->tsize));
     CE_TRY(hipMalloc(&e->L, E * sizeof(double)));
     CE_TRY(hipMalloc(&e->step, E * sizeof(int32_t)));
@@ -325,10 +408,17 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     CE_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_out), e->out_bytes));
     CE_TRY(hipMemset(e->d_out, 0, e->out_bytes));
     std::memset(e->h_out, 0, e->out_bytes);
-    CE_TRY(hipMemset(e->G, 0, E * P * e->tsize));
+    CE_TRY(hipMemset(e->G, 0, E * P * e->gsize));
     CE_TRY(hipMemset(e->L, 0, E * sizeof(double)));
     CE_TRY(hipMemset(e->step, 0, E * sizeof(int32_t)));
+    if (mlp) {
+        std::vector<float> x32(N * F);
+        for (size_t i = 0; i < N * F; ++i) x32[i] = static_cast<float>(features[i]);
+        CE_TRY(hipMemcpy(e->X, x32.data(), N * F * sizeof(float), hipMemcpyHostToDevice));
+        CE_TRY(hipMemcpy(e->label, labels, N * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
 #undef CE_TRY
+    if (!mlp) {
     // [rows | labels]: row-major rows padded to ce::row_stride elements (zeros
     // in the pad), then the int32 labels, in one buffer staged with one copy
     const size_t RS = ce::row_stride(cfg->n_features, static_cast<int>(e->tsize));
@@ -351,6 +441,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     e->staged = e->stage_bytes <= ce::kStageLimit;
     if (const char *ns = std::getenv("CE_NO_STAGE"))   // experiment switch: rows from L1/L2
         if (ns[0] == '1') e->staged = false;
+    }
     // Unseeded envs behave like np_random(None): os.urandom seeds.  The host
     // side normally seeds explicitly; default to seed = env index here.
     std::vector<uint64_t> seeds(E);
@@ -391,12 +482,33 @@ int ce_seed(ce_engine *e, const uint64_t *seeds, int32_t n) {
     if (n != e->cfg.num_envs) return fail(CE_EINVAL, "ce_seed: need one seed per env");
     const size_t E = n, P = e->P, N = e->cfg.n_rows;
     const bool with_perm = e->perm != nullptr;
+    if (e->mlp) {
+        std::vector<float> w0(E * P);
+        std::vector<int32_t> perm(E * N);
+        const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        const size_t nt = std::min<size_t>(hw, E);
+        std::vector<std::thread> pool;
+        for (size_t t = 0; t < nt; ++t)
+            pool.emplace_back([&, t] {
+                for (size_t i = t; i < E; i += nt)
+                    ce::reset_draws_mlp(seeds[i], e->cfg.n_features, e->cfg.n_hidden,
+                                        e->cfg.n_classes, static_cast<int>(N), &w0[i * P],
+                                        &perm[i * N]);
+            });
+        for (auto &th : pool) th.join();
+        CE_HIP(hipMemcpyAsync(e->W0, w0.data(), E * P * sizeof(float), hipMemcpyHostToDevice,
+                              e->stream));
+        CE_HIP(hipMemcpyAsync(e->perm, perm.data(), E * N * sizeof(int32_t),
+                              hipMemcpyHostToDevice, e->stream));
+        CE_HIP(hipStreamSynchronize(e->stream));
+        return CE_OK;
+    }
     std::vector<double> w0(E * P);
     std::vector<int32_t> perm(with_perm ? E * N : 0);
     for (size_t i = 0; i < E; ++i)
         ce::reset_draws(seeds[i], e->cfg.n_features, e->cfg.n_classes, static_cast<int>(N),
                         &w0[i * P], with_perm ? &perm[i * N] : nullptr);
-    int rc = upload_typed(e, e->W0, w0.data(), E * P);
+    int rc = upload_typed(e, e->W0, w0.data(), E * P, e->tsize);
     if (rc != CE_OK) return rc;
     if (with_perm)
         CE_HIP(hipMemcpyAsync(e->perm, perm.data(), E * N * sizeof(int32_t),
@@ -495,9 +607,9 @@ int ce_get_state(ce_engine *e, const ce_state *st) {
     const size_t E = e->cfg.num_envs, P = e->P, N = e->cfg.n_rows;
     int rc;
     CE_HIP(hipStreamSynchronize(e->stream));
-    if (st->weights && (rc = download_typed(e, st->weights, e->W, E * P)) != CE_OK) return rc;
-    if (st->grad_hist && (rc = download_typed(e, st->grad_hist, e->G, E * P)) != CE_OK) return rc;
-    if (st->init_weights && (rc = download_typed(e, st->init_weights, e->W0, E * P)) != CE_OK)
+    if (st->weights && (rc = download_typed(e, st->weights, e->W, E * P, e->tsize)) != CE_OK) return rc;
+    if (st->grad_hist && (rc = download_typed(e, st->grad_hist, e->G, E * P, e->gsize)) != CE_OK) return rc;
+    if (st->init_weights && (rc = download_typed(e, st->init_weights, e->W0, E * P, e->tsize)) != CE_OK)
         return rc;
     if (st->loss_hist) CE_HIP(hipMemcpy(st->loss_hist, e->L, E * sizeof(double), hipMemcpyDeviceToHost));
     if (st->step) CE_HIP(hipMemcpy(st->step, e->step, E * sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -517,9 +629,9 @@ int ce_set_state(ce_engine *e, const ce_state *st) {
     const size_t E = e->cfg.num_envs, P = e->P, N = e->cfg.n_rows;
     int rc;
     CE_HIP(hipStreamSynchronize(e->stream));
-    if (st->weights && (rc = upload_typed(e, e->W, st->weights, E * P)) != CE_OK) return rc;
-    if (st->grad_hist && (rc = upload_typed(e, e->G, st->grad_hist, E * P)) != CE_OK) return rc;
-    if (st->init_weights && (rc = upload_typed(e, e->W0, st->init_weights, E * P)) != CE_OK)
+    if (st->weights && (rc = upload_typed(e, e->W, st->weights, E * P, e->tsize)) != CE_OK) return rc;
+    if (st->grad_hist && (rc = upload_typed(e, e->G, st->grad_hist, E * P, e->gsize)) != CE_OK) return rc;
+    if (st->init_weights && (rc = upload_typed(e, e->W0, st->init_weights, E * P, e->tsize)) != CE_OK)
         return rc;
     if (st->loss_hist) CE_HIP(hipMemcpy(e->L, st->loss_hist, E * sizeof(double), hipMemcpyHostToDevice));
     if (st->step) CE_HIP(hipMemcpy(e->step, st->step, E * sizeof(int32_t), hipMemcpyHostToDevice));

@@ -20,13 +20,24 @@ using ce::fail;
 
 using MultiFn = void (*)(const ce::MultiArgs &, int grid, hipStream_t);
 
+// one lane per (env, agent): E groups of Group<P>::G lanes
 template <int P>
-void launch_multi_step(const ce::MultiArgs &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(ce::multi_step_kernel<P>, dim3(grid), dim3(ce::kMultiBlock), 0, s, a);
+int multi_grid(int E) {
+    const long lanes = static_cast<long>(E) * ce::Group<P>::G;
+    return static_cast<int>((lanes + ce::kMultiBlock - 1) / ce::kMultiBlock);
 }
 template <int P>
-void launch_multi_reset(const ce::MultiArgs &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(ce::multi_reset_kernel<P>, dim3(grid), dim3(ce::kMultiBlock), 0, s, a);
+void launch_multi_step(const ce::MultiArgs &a, int, hipStream_t s) {
+    // LDS stage of the observation rows: 4 waves x (64/G envs x P rows x 3H)
+    const size_t lds = a.H <= ce::kMultiStageH
+                           ? 4 * (64 / ce::Group<P>::G) * P * 3 * a.H * sizeof(float) : 0;
+    hipLaunchKernelGGL(ce::multi_step_kernel<P>, dim3(multi_grid<P>(a.E)), dim3(ce::kMultiBlock),
+                       lds, s, a);
+}
+template <int P>
+void launch_multi_reset(const ce::MultiArgs &a, int, hipStream_t s) {
+    hipLaunchKernelGGL(ce::multi_reset_kernel<P>, dim3(multi_grid<P>(a.E)),
+                       dim3(ce::kMultiBlock), 0, s, a);
 }
 
 struct MultiEntry {
@@ -45,8 +56,7 @@ struct ce_multi_engine {
     ce_multi_config cfg{};
     const MultiEntry *kern = nullptr;
     hipStream_t own_stream = nullptr, stream = nullptr;
-    float *init = nullptr;
-    int32_t *row_agent = nullptr;
+    int32_t agent_row[ce::kMultiMaxP] = {};   // output row of each agent (sorted names)
     float *theta = nullptr, *grad = nullptr, *hl = nullptr, *hg = nullptr, *hw = nullptr;
     double *al = nullptr, *ag = nullptr, *aw = nullptr;
     int32_t *step = nullptr;
@@ -81,8 +91,10 @@ ce::MultiArgs make_args(const ce_multi_engine *e, const float *act, const ce_mul
     a.H = e->cfg.max_history;
     a.max_batches = e->cfg.max_batches;
     a.auto_reset = e->cfg.auto_reset;
-    a.init = e->init;
-    a.row_agent = e->row_agent;
+    for (int i = 0; i < ce::kMultiMaxP; ++i) {
+        a.init[i] = i < e->cfg.n_params ? e->cfg.initial_points[i] : 0.0f;
+        a.agent_row[i] = e->agent_row[i];
+    }
     a.theta = e->theta;
     a.grad = e->grad;
     a.hl = e->hl;
@@ -186,8 +198,6 @@ int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out) {
     CE_TRY(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
     e->stream = e->own_stream;
     const size_t E = cfg->num_envs, P = cfg->n_params, H = cfg->max_history;
-    CE_TRY(hipMalloc(&e->init, P * sizeof(float)));
-    CE_TRY(hipMalloc(&e->row_agent, P * sizeof(int32_t)));
     CE_TRY(hipMalloc(&e->theta, P * E * sizeof(float)));
     CE_TRY(hipMalloc(&e->grad, P * E * sizeof(float)));
     CE_TRY(hipMalloc(&e->hl, ce::kRawHist * E * sizeof(float)));
@@ -217,8 +227,7 @@ int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out) {
     std::vector<int32_t> order(P);
     for (size_t i = 0; i < P; ++i) order[i] = static_cast<int32_t>(i);
     std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return names[x] < names[y]; });
-    CE_TRY(hipMemcpy(e->row_agent, order.data(), P * sizeof(int32_t), hipMemcpyHostToDevice));
-    CE_TRY(hipMemcpy(e->init, cfg->initial_points, P * sizeof(float), hipMemcpyHostToDevice));
+    for (size_t r = 0; r < P; ++r) e->agent_row[order[r]] = static_cast<int32_t>(r);
 #undef CE_TRY
     *out = e;
     return CE_OK;
@@ -228,7 +237,7 @@ void ce_multi_destroy(ce_multi_engine *e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->graph) (void)hipGraphExecDestroy(e->graph);
-    void *dev[] = {e->init, e->row_agent, e->theta, e->grad, e->hl, e->hg, e->hw,
+    void *dev[] = {e->theta, e->grad, e->hl, e->hg, e->hw,
                    e->al, e->ag, e->aw, e->step, e->d_act, e->d_out};
     for (void *p : dev)
         if (p) (void)hipFree(p);
@@ -328,10 +337,7 @@ int ce_multi_get_state(ce_multi_engine *e, float *theta, int32_t *step) {
     const size_t E = e->cfg.num_envs, P = e->cfg.n_params;
     CE_HIP(hipStreamSynchronize(e->stream));
     if (theta) {
-        std::vector<float> soa(P * E);
-        CE_HIP(hipMemcpy(soa.data(), e->theta, P * E * sizeof(float), hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < E; ++i)
-            for (size_t p = 0; p < P; ++p) theta[i * P + p] = soa[p * E + i];
+        CE_HIP(hipMemcpy(theta, e->theta, P * E * sizeof(float), hipMemcpyDeviceToHost));
     }
     if (step) CE_HIP(hipMemcpy(step, e->step, E * sizeof(int32_t), hipMemcpyDeviceToHost));
     return CE_OK;

@@ -17,11 +17,17 @@
 //     early stop at loss > 1e4 with penalty; 14-key info (multioptlrs.py:97-127)
 //   auto-reset on done                    concurrentvecenv.py:37 (any(done) on the agent list)
 //
-// Mapping: one thread per env (P is a handful of agents).  State is struct-
-// of-arrays [field][E] so a wave's 64 envs read and write coalesced lines.
-// Rings: the raw history keeps 5 entries (multioptlrs.py:42-45), slot
-// step % 5; the adjusted history keeps H entries, slot (step - 1) % H;
-// a slot not written since the last reset reads as the reset zero.
+// Mapping: one lane per (env, agent).  An env's agents are a group of G lanes
+// (G = P rounded up to a power of two; lanes i >= P idle), so a wave holds
+// 64/G envs and every per-env quantity is a shuffle reduction inside the
+// group.  Lane i is AGENT i; its output row is agent_row[i] (the sorted-name
+// order, which differs from the agent order once P >= 11).  Per-agent state
+// is [slot][E][P] so a group's P values are contiguous and a wave's loads and
+// stores are coalesced.  Rings: the raw history keeps 5 entries
+// (multioptlrs.py:42-45), slot step % 5; the adjusted history keeps H
+// entries, slot (step - 1) % H; a slot not written since the last reset
+// reads as the reset zero.  The wave's observation rows are one contiguous
+// block of the output: they are assembled in LDS and stored lane-contiguous.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -31,20 +37,22 @@ namespace ce {
 
 constexpr int kRawHist = 5;
 constexpr int kMultiBlock = 256;
-constexpr int kMultiInfo = 14;   // info keys, order in include/custom_envs_amd.h
+constexpr int kMultiInfo = 14;     // info keys, order in include/custom_envs_amd.h
+constexpr int kMultiMaxP = 16;
+constexpr int kMultiStageH = 20;   // LDS-staged observation rows up to this H
 
 struct MultiArgs {
     int E, H, max_batches, auto_reset;
-    const float *init;       // [P] initial points
-    const int32_t *row_agent;// [P] agent index of row r (sorted agent names)
-    float *theta;            // [P][E]
-    float *grad;             // [P][E] gradient at theta (newest raw entry)
+    float init[kMultiMaxP];      // initial points (agent order)
+    int agent_row[kMultiMaxP];   // output row of agent i within its env
+    float *theta;            // [E][P]
+    float *grad;             // [E][P] gradient at theta (newest raw entry)
     float *hl;               // [5][E]
-    float *hg;               // [5][P][E]
-    float *hw;               // [5][P][E]
+    float *hg;               // [5][E][P]
+    float *hw;               // [5][E][P]
     double *al;              // [H][E]
-    double *ag;              // [H][P][E]
-    double *aw;              // [H][P][E]
+    double *ag;              // [H][E][P]
+    double *aw;              // [H][E][P]
     int32_t *step;           // [E]
     const float *act;        // [E][P] rows
     float *obs;              // [E][P][3H] rows
@@ -54,23 +62,38 @@ struct MultiArgs {
     int32_t *episode_len;    // [E]
 };
 
+template <int P>
+struct Group {
+    static constexpr int G = P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : 16;
+};
+
+template <int G, typename T>
+__device__ __forceinline__ T group_sum(T v) {
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off, G);
+    return v;
+}
+
 // Sum of Rosenbrock over coordinate pairs in float32, with TF1's autodiff
 // order for the gradient: dL/dy = 200 d, dL/dx = -(2 (200 d)) x - 2 (1 - x),
-// d = y - x^2.  Contraction is off so every product rounds as in the oracle.
+// d = y - x^2; the loss sums the pairs left to right.  Lane i holds agent i;
+// its pair partner is lane i ^ 1.  Contraction is off so every product
+// rounds as in the oracle.
 template <int P>
-__device__ __forceinline__ void rosenbrock_pairs(const float (&th)[P], float (&g)[P], float &loss) {
+__device__ __forceinline__ void rosenbrock_lane(float th, int i, float &g, float &loss) {
 #pragma clang fp contract(off)
+    constexpr int G = Group<P>::G;
+    const float other = __shfl_xor(th, 1, G);
+    const bool is_x = (i & 1) == 0;
+    const float x = is_x ? th : other, y = is_x ? other : th;
+    const float d = y - x * x;
+    const float r = 1.0f - x;
+    const float term = 100.0f * (d * d) + r * r;
+    const float t = 200.0f * d;
+    g = is_x ? -((2.0f * t) * x) - 2.0f * r : t;
     loss = 0.0f;
 #pragma unroll
-    for (int k = 0; k < P; k += 2) {
-        const float x = th[k], y = th[k + 1];
-        const float d = y - x * x;
-        const float r = 1.0f - x;
-        loss = loss + (100.0f * (d * d) + r * r);
-        const float t = 200.0f * d;
-        g[k] = -((2.0f * t) * x) - 2.0f * r;
-        g[k + 1] = t;
-    }
+    for (int p = 0; p < P / 2; ++p) loss = loss + __shfl(term, 2 * p, G);
 }
 
 // numpy.nan_to_num of a / |b| in float64.
@@ -86,99 +109,101 @@ __device__ __forceinline__ double clip100(double v) {
     return v < -100.0 ? -100.0 : (v > 100.0 ? 100.0 : v);
 }
 
+// Reset agent i of env e (MultiOptLRs.base_reset, multioptlrs.py:66-78): the
+// problem back at its initial point (th0, with gradient g0 and loss l0 from
+// rosenbrock_lane, evaluated by every lane of the group), the raw history
+// holding that point only, the adjusted history zero.
 template <int P>
-__device__ __forceinline__ void multi_reset_env(const MultiArgs &a, int e) {
+__device__ __forceinline__ void multi_store_reset(const MultiArgs &a, size_t e, int i, float th0,
+                                                  float g0, float l0) {
     const size_t E = a.E;
-    float th[P], g[P], loss;
-#pragma unroll
-    for (int i = 0; i < P; ++i) th[i] = a.init[i];
-    rosenbrock_pairs<P>(th, g, loss);
     for (int s = 0; s < kRawHist; ++s) {
-        a.hl[s * E + e] = s == 0 ? loss : 0.0f;
-#pragma unroll
-        for (int i = 0; i < P; ++i) {
-            a.hg[(s * P + i) * E + e] = s == 0 ? g[i] : 0.0f;
-            a.hw[(s * P + i) * E + e] = s == 0 ? th[i] : 0.0f;
-        }
+        a.hg[(s * E + e) * P + i] = s == 0 ? g0 : 0.0f;
+        a.hw[(s * E + e) * P + i] = s == 0 ? th0 : 0.0f;
+        if (i == 0) a.hl[s * E + e] = s == 0 ? l0 : 0.0f;
     }
     for (int s = 0; s < a.H; ++s) {
-        a.al[s * E + e] = 0.0;
-#pragma unroll
-        for (int i = 0; i < P; ++i) {
-            a.ag[(s * P + i) * E + e] = 0.0;
-            a.aw[(s * P + i) * E + e] = 0.0;
-        }
+        a.ag[(s * E + e) * P + i] = 0.0;
+        a.aw[(s * E + e) * P + i] = 0.0;
+        if (i == 0) a.al[s * E + e] = 0.0;
     }
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-        a.theta[i * E + e] = th[i];
-        a.grad[i * E + e] = g[i];
-    }
-    a.step[e] = 0;
+    a.theta[e * P + i] = th0;
+    a.grad[e * P + i] = g0;
+    if (i == 0) a.step[e] = 0;
 }
 
 template <int P>
 __global__ __launch_bounds__(kMultiBlock) void multi_reset_kernel(MultiArgs a) {
-    const int e = blockIdx.x * kMultiBlock + threadIdx.x;
-    if (e >= a.E) return;
-    multi_reset_env<P>(a, e);
+    constexpr int G = Group<P>::G;
+    const size_t gt = static_cast<size_t>(blockIdx.x) * kMultiBlock + threadIdx.x;
+    const size_t e = gt / G;
+    const int i = static_cast<int>(gt % G);
+    const bool on = e < static_cast<size_t>(a.E) && i < P;
+    const float th0 = i < P ? a.init[i] : 0.0f;
+    float g0, l0;
+    rosenbrock_lane<P>(th0, i, g0, l0);
+    if (!on) return;
+    multi_store_reset<P>(a, e, i, th0, g0, l0);
     const int row = 3 * a.H;
-    for (int k = 0; k < P * row; ++k) a.obs[static_cast<size_t>(e) * P * row + k] = -1.0f;
+    float *o = a.obs + (e * P + a.agent_row[i]) * row;
+    for (int k = 0; k < row; ++k) o[k] = -1.0f;
 }
 
 template <int P>
 __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
 #pragma clang fp contract(off)
-    const int e = blockIdx.x * kMultiBlock + threadIdx.x;
-    if (e >= a.E) return;
+    constexpr int G = Group<P>::G;
+    extern __shared__ float stage[];          // [4 waves][64 / G * P * 3H] when H <= kMultiStageH
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t gt = static_cast<size_t>(blockIdx.x) * kMultiBlock + threadIdx.x;
+    const size_t e = gt / G;
+    const int i = static_cast<int>(gt % G);
     const size_t E = a.E;
+    const bool env_ok = e < E;
+    const bool on = env_ok && i < P;
     const int H = a.H;
-    const int s = a.step[e] + 1;
+    const int row = 3 * H;
+    const size_t ec = env_ok ? e : 0;          // clamp so idle lanes read valid memory
+    const int ic = i < P ? i : 0;
+    const int r = a.agent_row[ic];
 
-    // ---- update (multioptlrs.py:81-87): rows -> agents, lr = 10^(a - 4)
-    float th[P], g[P], lr[P];
-#pragma unroll
-    for (int r = 0; r < P; ++r) {
-        const int i = a.row_agent[r];
-        // numpy float32 10 ** (a - 4): the exponent rounds to float32 first;
-        // the power is taken in float64 and rounded once (correctly rounded
-        // but for ties far below float32 resolution)
-        const float x = a.act[static_cast<size_t>(e) * P + r] - 4.0f;
-        lr[i] = static_cast<float>(pow(10.0, static_cast<double>(x)));
-    }
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-        th[i] = a.theta[i * E + e];
-        g[i] = a.grad[i * E + e];
-    }
-#pragma unroll
-    for (int i = 0; i < P; ++i) th[i] = th[i] - g[i] * lr[i];
-    float loss;
-    rosenbrock_pairs<P>(th, g, loss);
+    const int s = a.step[ec] + 1;
+    // ---- update (multioptlrs.py:81-87), lr = 10^(a - 4): the exponent rounds
+    // to float32 first; the power is taken in float64 and rounded once
+    const float x = a.act[ec * P + r] - 4.0f;
+    const float lr = static_cast<float>(pow(10.0, static_cast<double>(x)));
+    const float th0 = a.theta[ec * P + ic];
+    const float g0 = a.grad[ec * P + ic];
+    const float th = th0 - g0 * lr;
+    float g, loss;
+    rosenbrock_lane<P>(th, i, g, loss);
 
     // ---- raw history append, observation v3 against the previous entry
     const int slot = s % kRawHist, prev = (s - 1) % kRawHist;
-    const double l_prev = a.hl[prev * E + e];
-    a.hl[slot * E + e] = loss;
+    const double l_prev = a.hl[prev * E + ec];
+    const float gp = a.hg[(prev * E + ec) * P + ic];
+    const float wp = a.hw[(prev * E + ec) * P + ic];
     const double adj_l = ratio(loss, l_prev);
-    double adj_w[P], adj_g[P];
-    double gdiff = 0.0;
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-        const float gp = a.hg[(prev * P + i) * E + e];
-        const float wp = a.hw[(prev * P + i) * E + e];
-        adj_g[i] = ratio(g[i], gp);
-        adj_w[i] = ratio(th[i], wp);
-        gdiff += fabs(static_cast<double>(g[i]) - static_cast<double>(gp));
-        a.hg[(slot * P + i) * E + e] = g[i];
-        a.hw[(slot * P + i) * E + e] = th[i];
+    const double adj_g = ratio(g, gp);
+    const double adj_w = ratio(th, wp);
+    // info sums over the raw ring: this step's entry from registers, the
+    // other four from memory (read before this step's slot is overwritten)
+    double lsum = loss, gsum = g;
+    for (int k = 0; k < kRawHist; ++k) {
+        if (k == slot) continue;
+        lsum += a.hl[k * E + ec];
+        gsum += a.hg[(k * E + ec) * P + ic];
     }
     const int aslot = (s - 1) % H;
-    a.al[aslot * E + e] = adj_l;
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-        a.ag[(aslot * P + i) * E + e] = adj_g[i];
-        a.aw[(aslot * P + i) * E + e] = adj_w[i];
+    if (on) {
+        a.hg[(slot * E + e) * P + i] = g;
+        a.hw[(slot * E + e) * P + i] = th;
+        a.ag[(aslot * E + e) * P + i] = adj_g;
+        a.aw[(aslot * E + e) * P + i] = adj_w;
+        if (i == 0) {
+            a.hl[slot * E + e] = loss;
+            a.al[aslot * E + e] = adj_l;
+        }
     }
 
     // ---- reward v6 + termination (multioptlrs.py:102-107)
@@ -189,78 +214,84 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
         terminal = true;
         reward -= static_cast<double>(a.max_batches - s);
     }
-
-    // ---- observations: per agent [w~ (H, newest first) | l~ (H) | g~ (H)]
-    const int row = 3 * H;
-    float *obs = a.obs + static_cast<size_t>(e) * P * row;
-    double st_abs = 0.0;
     const bool wipe = terminal && a.auto_reset;
+
+    // ---- observation row of agent i: [w~ (H, newest first) | l~ (H) | g~ (H)]
+    const bool staged = H <= kMultiStageH;
+    const int span = 64 / G * P * row;       // floats of one wave's env block
+    float *lds = stage + wave * span;
+    float *dst = staged ? lds + ((lane / G) * P + r) * row : a.obs + (ec * P + r) * row;
+    double st_abs = 0.0;
     for (int k = 0; k < H; ++k) {
-        const bool live = k < s;                    // older slots are reset zeros
-        const int sl = ((s - 1 - k) % H + H) % H;
-        const double lk = live ? a.al[sl * E + e] : 0.0;
-        st_abs += P * fabs(lk);
-#pragma unroll
-        for (int r = 0; r < P; ++r) {
-            const int i = a.row_agent[r];
-            const double wk = live ? a.aw[(sl * P + i) * E + e] : 0.0;
-            const double gk = live ? a.ag[(sl * P + i) * E + e] : 0.0;
-            st_abs += fabs(wk) + fabs(gk);
-            float *o = obs + r * row;
-            o[k] = wipe ? -1.0f : static_cast<float>(clip100(wk) - 1.0);
-            o[H + k] = wipe ? -1.0f : static_cast<float>(clip100(lk) - 1.0);
-            o[2 * H + k] = wipe ? -1.0f : static_cast<float>(clip100(gk) - 1.0);
+        double wk = adj_w, gk = adj_g, lk = adj_l;  // k = 0: this step's entry
+        if (k > 0) {
+            const bool live = k < s;                // older slots are reset zeros
+            const int sl = ((s - 1 - k) % H + H) % H;
+            wk = live ? a.aw[(sl * E + ec) * P + ic] : 0.0;
+            gk = live ? a.ag[(sl * E + ec) * P + ic] : 0.0;
+            lk = live ? a.al[sl * E + ec] : 0.0;
+        }
+        st_abs += fabs(wk) + fabs(gk) + fabs(lk);
+        if (on) {
+            dst[k] = wipe ? -1.0f : static_cast<float>(clip100(wk) - 1.0);
+            dst[H + k] = wipe ? -1.0f : static_cast<float>(clip100(lk) - 1.0);
+            dst[2 * H + k] = wipe ? -1.0f : static_cast<float>(clip100(gk) - 1.0);
         }
     }
-
-    // ---- info (multioptlrs.py:112-127), float64 arithmetic
-    double wsum = 0.0, amean = 0.0, gsum = 0.0, lsum = 0.0, adjg = 0.0;
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-        wsum += fabs(static_cast<double>(th[i]));
-        amean += lr[i];
-        adjg += fabs(adj_g[i]);
-    }
-    amean /= P;
-    double avar = 0.0;
-#pragma unroll
-    for (int i = 0; i < P; ++i) avar += (lr[i] - amean) * (lr[i] - amean);
-    for (int k = 0; k < kRawHist; ++k) {
-        lsum += a.hl[k * E + e];
-#pragma unroll
-        for (int i = 0; i < P; ++i) gsum += a.hg[(k * P + i) * E + e];
-    }
-    float *info = a.info + static_cast<size_t>(e) * kMultiInfo;
-    info[0] = terminal ? loss : __builtin_nanf("");          // loss (None -> NaN)
-    info[1] = loss;                                           // batch_loss
-    info[2] = static_cast<float>(wsum / P);                   // weights_mean
-    info[3] = static_cast<float>(wsum);                       // weights_sum
-    info[4] = static_cast<float>(amean);                      // actions_mean
-    info[5] = static_cast<float>(sqrt(avar / P));             // actions_std
-    info[6] = static_cast<float>(st_abs / (P * row));         // states_mean
-    info[7] = static_cast<float>(st_abs);                     // states_sum
-    info[8] = static_cast<float>(gsum / (kRawHist * P));      // grads_mean
-    info[9] = static_cast<float>(gsum);                       // grads_sum
-    info[10] = static_cast<float>(lsum / kRawHist);           // loss_mean
-    info[11] = static_cast<float>(adj_l);                     // adjusted_loss
-    info[12] = static_cast<float>(adjg / P);                  // adjusted_grad
-    info[13] = static_cast<float>(gdiff / P);                 // grad_diff
-    a.episode_len[e] = s;
-#pragma unroll
-    for (int r = 0; r < P; ++r) {
-        a.reward[static_cast<size_t>(e) * P + r] = static_cast<float>(reward);
-        a.done[static_cast<size_t>(e) * P + r] = terminal ? 1 : 0;
+    if (staged) {
+        // the wave's rows are obs[e_first * P * row ...] contiguous
+        __syncthreads();                        // every thread gets here (no early exit)
+        const size_t e_first = (static_cast<size_t>(blockIdx.x) * kMultiBlock + wave * 64) / G;
+        const size_t envs = e_first < E ? (E - e_first < static_cast<size_t>(64 / G)
+                                               ? E - e_first : static_cast<size_t>(64 / G))
+                                        : 0;
+        const int n = static_cast<int>(envs) * P * row;
+        float *out = a.obs + e_first * P * row;
+        for (int q = lane; q < n; q += 64) out[q] = lds[q];
     }
 
-    if (wipe) {
-        multi_reset_env<P>(a, e);
-    } else {
-#pragma unroll
-        for (int i = 0; i < P; ++i) {
-            a.theta[i * E + e] = th[i];
-            a.grad[i * E + e] = g[i];
+    // ---- info (multioptlrs.py:112-127), float64 group reductions
+    const double mine = on ? 1.0 : 0.0;
+    const double wsum = group_sum<G>(mine * fabs(static_cast<double>(th)));
+    const double amean = group_sum<G>(mine * static_cast<double>(lr)) / P;
+    const double dev = static_cast<double>(lr) - amean;
+    const double avar = group_sum<G>(mine * dev * dev) / P;
+    const double adjg = group_sum<G>(mine * fabs(adj_g)) / P;
+    const double gdiff = group_sum<G>(mine * fabs(static_cast<double>(g) - static_cast<double>(gp))) / P;
+    const double gsum_all = group_sum<G>(mine * gsum);
+    const double st_all = group_sum<G>(mine * st_abs);
+    if (on) {
+        if (i == 0) {
+            float *info = a.info + e * kMultiInfo;
+            info[0] = terminal ? loss : __builtin_nanf("");          // loss (None -> NaN)
+            info[1] = loss;                                           // batch_loss
+            info[2] = static_cast<float>(wsum / P);                   // weights_mean
+            info[3] = static_cast<float>(wsum);                       // weights_sum
+            info[4] = static_cast<float>(amean);                      // actions_mean
+            info[5] = static_cast<float>(sqrt(avar));                 // actions_std
+            info[6] = static_cast<float>(st_all / (P * row));         // states_mean
+            info[7] = static_cast<float>(st_all);                     // states_sum
+            info[8] = static_cast<float>(gsum_all / (kRawHist * P));  // grads_mean
+            info[9] = static_cast<float>(gsum_all);                   // grads_sum
+            info[10] = static_cast<float>(lsum / kRawHist);           // loss_mean
+            info[11] = static_cast<float>(adj_l);                     // adjusted_loss
+            info[12] = static_cast<float>(adjg);                      // adjusted_grad
+            info[13] = static_cast<float>(gdiff);                     // grad_diff
+            a.episode_len[e] = s;
         }
-        a.step[e] = s;
+        a.reward[e * P + r] = static_cast<float>(reward);
+        a.done[e * P + r] = terminal ? 1 : 0;
+    }
+
+    const float th_init = i < P ? a.init[i] : 0.0f;
+    float g_init, l_init;
+    rosenbrock_lane<P>(th_init, i, g_init, l_init);     // all lanes: it shuffles
+    if (wipe && on) {
+        multi_store_reset<P>(a, e, i, th_init, g_init, l_init);
+    } else if (on) {
+        a.theta[e * P + i] = th;
+        a.grad[e * P + i] = g;
+        if (i == 0) a.step[e] = s;
     }
 }
 

@@ -18,6 +18,7 @@ from custom_envs_amd._native import CeConfig, CeOutputs, CeState, check
 
 PRECISIONS = {'f64': _native.CE_F64, 'float64': _native.CE_F64,
               'f32': _native.CE_F32, 'float32': _native.CE_F32}
+MODELS = {'linear': _native.CE_PROBLEM_SOFTMAX, 'mlp': _native.CE_PROBLEM_MLP}
 
 
 def normalize_seed(seed):
@@ -46,7 +47,14 @@ class OptimizeEngine:
     """E Optimize-v0 environments advanced in lock step on one GPU."""
 
     def __init__(self, features, targets, num_envs, batch_size=None, max_steps=40,
-                 precision='f64', device=0, auto_reset=True):
+                 precision=None, device=0, auto_reset=True, model='linear', hidden=64):
+        """``model``: 'linear' (the build-defined ModelNumpy softmax classifier,
+        float64 by default) or 'mlp' (config 3: F -> hidden relu -> K softmax,
+        float32)."""
+        if model not in MODELS:
+            raise ValueError('model must be one of %s' % sorted(MODELS))
+        if precision is None:
+            precision = 'f32' if model == 'mlp' else 'f64'
         lib = _native.load()
         features = np.ascontiguousarray(features, dtype=np.float64)
         labels, n_classes = labels_from_targets(targets)
@@ -58,12 +66,14 @@ class OptimizeEngine:
         self.batch_size = n_rows if batch_size is None else int(batch_size)
         self.max_steps = int(max_steps)
         self.precision = precision
+        self.model, self.hidden = model, int(hidden)
         self.device = int(device)
-        cfg = CeConfig(abi_version=_native.ABI_VERSION, problem=_native.CE_PROBLEM_SOFTMAX,
+        cfg = CeConfig(abi_version=_native.ABI_VERSION, problem=MODELS[model],
                        precision=PRECISIONS[precision], device=self.device,
                        num_envs=self.num_envs, n_rows=n_rows, n_features=n_features,
                        n_classes=n_classes, batch_size=self.batch_size,
-                       max_steps=self.max_steps, auto_reset=1 if auto_reset else 0)
+                       max_steps=self.max_steps, auto_reset=1 if auto_reset else 0,
+                       n_hidden=self.hidden if model == 'mlp' else 0)
         self._labels = np.ascontiguousarray(labels, dtype=np.int32)
         handle = ctypes.c_void_p()
         check(lib.ce_create(ctypes.byref(cfg), features.ctypes.data, self._labels.ctypes.data,

@@ -39,12 +39,15 @@ class Optimize(Env):
     metadata = {'render.modes': []}
 
     def __init__(self, data_set='gaussians_256x10', batch_size=None, n_of_steps=None,
-                 max_steps=40, precision='f64', device=0):
+                 max_steps=40, precision=None, device=0, model='linear', hidden=64):
+        """``model='mlp'`` swaps the classifier for the config-3 MLP
+        (F -> hidden relu -> K, float32)."""
         from custom_envs_amd.engine import OptimizeEngine
         features, targets = resolve_dataset(data_set, batch_size)
         self.engine = OptimizeEngine(features, targets, 1, batch_size=batch_size,
                                      max_steps=max_steps, precision=precision,
-                                     device=device, auto_reset=False)
+                                     device=device, auto_reset=False, model=model,
+                                     hidden=hidden)
         self.current_step = 0
         self.observation_space, self.action_space = optimize_spaces(self.engine.act_dim)
         self.seed()

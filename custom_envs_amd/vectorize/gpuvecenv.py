@@ -52,12 +52,13 @@ class GPUVecEnv:
     """E Optimize-v0 envs on one MI355X behind the SB VecEnv interface."""
 
     def __init__(self, num_envs, data_set='gaussians_256x10', batch_size=None,
-                 n_of_steps=None, max_steps=40, precision='f64', device=0, seed=None):
+                 n_of_steps=None, max_steps=40, precision=None, device=0, seed=None,
+                 model='linear', hidden=64):
         from custom_envs_amd.engine import OptimizeEngine
         features, targets = resolve_dataset(data_set, batch_size)
         self.engine = OptimizeEngine(features, targets, num_envs, batch_size=batch_size,
                                      max_steps=max_steps, precision=precision, device=device,
-                                     auto_reset=True)
+                                     auto_reset=True, model=model, hidden=hidden)
         self.num_envs = int(num_envs)
         self.observation_space, self.action_space = optimize_spaces(self.engine.act_dim)
         self.current_step = np.zeros(self.num_envs, np.int64)

@@ -8,7 +8,8 @@
  *   ce_create      Optimize.__init__            custom_envs/envs/optimize.py:40-56
  *                  + ConcurrentVecEnv.__init__   custom_envs/vectorize/concurrentvecenv.py:77-95
  *   ce_seed        BaseEnvironment.seed          custom_envs/envs/baseenvironment.py:20-28
- *   ce_seed_draws  Optimize.base_reset draws     custom_envs/envs/optimize.py:63-64
+ *   ce_seed_draws / ce_seed_draws_mlp
+ *                  Optimize.base_reset draws     custom_envs/envs/optimize.py:63-64
  *                  (model.reset then sequence.shuffle under use_random_state,
  *                   custom_envs/utils/utils_math.py:9-22)
  *   ce_reset       ConcurrentVecEnv.reset        custom_envs/vectorize/concurrentvecenv.py:109-113
@@ -59,7 +60,7 @@
 extern "C" {
 #endif
 
-#define CE_ABI_VERSION 1
+#define CE_ABI_VERSION 2
 
 typedef struct ce_engine ce_engine;
 
@@ -74,7 +75,11 @@ typedef enum ce_status {
 
 typedef enum ce_problem {
     /* softmax classifier without bias (the missing ModelNumpy) */
-    CE_PROBLEM_SOFTMAX = 0
+    CE_PROBLEM_SOFTMAX = 0,
+    /* F -> n_hidden (relu) -> K softmax MLP, float32 (OptimizeNN network,
+       custom_envs/problems/optimize_nn.py:35-52);
+       flat parameters [W1 (F,H) | b1 | W2 (H,K) | b2]; CE_F32 only */
+    CE_PROBLEM_MLP = 1
 } ce_problem;
 
 typedef enum ce_precision {
@@ -99,9 +104,12 @@ typedef struct ce_config {
     int32_t max_steps;   /* episode length, optimize.py:102-103 (40)        */
     int32_t auto_reset;  /* 1: VecEnv auto-reset on done (utils_venv.py:31);
                             0: single gym.Env (baseenvironment.py:30-41)   */
+    int32_t n_hidden;    /* CE_PROBLEM_MLP hidden units (create_neural_net
+                            layers, utils_tf.py:74-86); ignored otherwise  */
 } ce_config;
 
-/* Per-step outputs, one row per env.  obs is [E][2P+1] with P = F*K. */
+/* Per-step outputs, one row per env.  obs is [E][2P+1] with P the problem's
+   parameter count (F*K for the softmax classifier). */
 typedef struct ce_outputs {
     float *obs;        /* concat(wght_hist[idx], loss_hist[idx], grad_hist[idx]) */
     float *reward;     /* -loss (minibatch, after the update)                */
@@ -138,6 +146,11 @@ int ce_seed(ce_engine *eng, const uint64_t *seeds, int32_t n);
 /* Host-only: the (W0, perm) that every reset of a seed draws.  No GPU. */
 int ce_seed_draws(uint64_t seed, int32_t n_features, int32_t n_classes,
                   int32_t n_rows, double *init_weights, int32_t *perm);
+/* Host-only, CE_PROBLEM_MLP: glorot-uniform W1 then W2 (float32, zero
+   biases, flat order) then the row permutation.  No GPU. */
+int ce_seed_draws_mlp(uint64_t seed, int32_t n_features, int32_t n_hidden,
+                      int32_t n_classes, int32_t n_rows, float *init_weights,
+                      int32_t *perm);
 
 int ce_reset(ce_engine *eng, const ce_outputs *out, uint32_t flags);
 int ce_step(ce_engine *eng, const float *actions /* [E][P] */,

@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 from oracle.data import gaussians
-from oracle.optimize import Optimize, initial_draws
+from oracle.optimize import Optimize, initial_draws, initial_draws_mlp
 from oracle.seeding import seed_key
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -116,6 +116,64 @@ def rollout_multi(ndims, max_batches, max_history, steps, action_seed, low=1.0, 
     return out
 
 
+MLP_KEEP = (0, 1, 19, 39, 40, 44)      # steps whose full obs / weights are stored
+
+
+def mlp_dataset(n_rows=128, n_features=16, n_classes=10):
+    """Small MLP fixture problem: uniform features, argmax((X - 1/2) T) labels."""
+    features = np.random.RandomState(2).rand(n_rows, n_features)
+    proj = np.random.RandomState(3).normal(size=(n_features, n_classes))
+    targets = np.eye(n_classes)[np.argmax((features - 0.5) @ proj, axis=1)]
+    return features, targets
+
+
+def mlp_actions(action_seed, steps, n_params):
+    return np.random.RandomState(action_seed).normal(0, 1e-3, (steps, n_params)).astype(
+        np.float32)
+
+
+def rollout_mlp(features, targets, seed, steps=45, action_seed=77, hidden=64):
+    """Optimize over the A12 MLP, B = 32, VecEnv auto-reset (utils_venv.py:31)."""
+    env = Optimize(features, targets, batch_size=32, model='mlp', hidden=hidden)
+    env.seed(seed)
+    first = env.reset()
+    P = env.model.size
+    actions = mlp_actions(action_seed, steps, P)
+    rec = {k: [] for k in ('reward', 'done', 'objective', 'accuracy', 'ep_len', 'loss_obs',
+                           'obs', 'weights')}
+    for t in range(steps):
+        obs, reward, done, info = env.step(actions[t])
+        rec['ep_len'].append(info['episode']['l'])
+        weights = env.model.weights.copy()
+        if done:
+            obs = env.reset()
+        rec['reward'].append(reward)
+        rec['done'].append(done)
+        rec['objective'].append(info['objective'])
+        rec['accuracy'].append(info['accuracy'])
+        rec['loss_obs'].append(obs[P])
+        if t in MLP_KEEP:
+            rec['obs'].append(obs.astype(np.float32))
+            rec['weights'].append(weights)
+    out = {k: np.array(v) for k, v in rec.items()}
+    out['reset_obs'] = first.astype(np.float32)
+    out['init_weights'] = initial_draws_mlp(seed, features.shape[1], hidden,
+                                            targets.shape[1], len(features))[0]
+    out['seed'] = np.array(seed)
+    out['action_seed'] = np.array(action_seed)
+    out['keep'] = np.array(MLP_KEEP)
+    return out
+
+
+def write_mlp():
+    features, targets = mlp_dataset()
+    np.savez_compressed(os.path.join(GOLDEN, 'mlp_data_128x16.npz'), features=features,
+                        targets=targets)
+    for seed in (5, 6):
+        rec = rollout_mlp(features, targets, seed, action_seed=77 + seed)
+        np.savez_compressed(os.path.join(GOLDEN, 'optimize_mlp_s%d.npz' % seed), **rec)
+
+
 def write_multi():
     # (name, ndims, max_batches, max_history, steps, seed, action range):
     # stable learning rates (10^-5..10^-3.5), the configs' 10^-3..10^-1
@@ -134,6 +192,7 @@ def main():
     write_seeding(features)
     write_rollouts(features, targets)
     write_multi()
+    write_mlp()
 
 
 if __name__ == '__main__':

@@ -98,3 +98,35 @@ def test_engine_without_gpu_fails_loudly(lr_dataset):
     from custom_envs_amd.engine import OptimizeEngine
     with pytest.raises(_native.NativeEngineError):
         OptimizeEngine(*lr_dataset, num_envs=2)
+
+
+@pytest.mark.parametrize('seed', [0, 9, 2**40 + 3])
+def test_native_mlp_seeding_against_live_numpy(seed):
+    """glorot-uniform W1, W2 (float32) then the permutation, as the oracle's
+    ModelMLP.reset + sequence.shuffle draw them under use_random_state."""
+    from oracle.optimize import initial_draws_mlp
+    lib = _native.load()
+    F, H, K, N = 24, 64, 10, 200
+    w_ref, p_ref = initial_draws_mlp(seed, F, H, K, N)
+    w0 = np.zeros(F * H + H + H * K + K, np.float32)
+    perm = np.zeros(N, np.int32)
+    _native.check(lib.ce_seed_draws_mlp(seed, F, H, K, N, w0.ctypes.data, perm.ctypes.data),
+                  'draw')
+    assert np.array_equal(w0, w_ref) and np.array_equal(perm, p_ref)
+
+
+@pytest.mark.parametrize('change', [dict(n_hidden=32), dict(batch_size=16),
+                                    dict(n_features=20), dict(n_classes=17),
+                                    dict(precision=_native.CE_F64)])
+def test_unsupported_mlp_shape_is_loud(change):
+    lib = _native.load()
+    base = dict(abi_version=_native.ABI_VERSION, problem=_native.CE_PROBLEM_MLP,
+                precision=_native.CE_F32, num_envs=1, n_rows=128, n_features=16,
+                n_classes=10, batch_size=32, max_steps=40, n_hidden=64)
+    base.update(change)
+    cfg = _native.CeConfig(**base)
+    x = np.zeros((128, base['n_features']))
+    y = np.zeros(128, np.int32)
+    handle = ctypes.c_void_p()
+    assert lib.ce_create(ctypes.byref(cfg), x.ctypes.data, y.ctypes.data,
+                         ctypes.byref(handle)) == _native.CE_EUNSUPPORTED

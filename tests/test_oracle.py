@@ -120,3 +120,41 @@ def test_np_random_contract():
     assert seed == 5 and isinstance(rng, npr.RandomState)
     with pytest.raises(ValueError):
         np_random(-1)
+
+
+def test_mlp_backprop_matches_torch_autograd():
+    """The oracle's float32 MLP gradient (A12) against float64 torch autograd of
+    sum_i -log(P_i + 1e-16) . Y_i (the tf.gradients of the per-sample loss
+    vector, optimize_nn.py:48-52)."""
+    import torch
+    from oracle.gen_golden import mlp_dataset
+    from oracle.optimize import ModelMLP, initial_draws_mlp
+    features, targets = mlp_dataset()
+    model = ModelMLP(16, 10, 64)
+    model.set_weights(initial_draws_mlp(4, 16, 64, 10, 128)[0])
+    x32, y32 = features[:32].astype(np.float32), targets[:32].astype(np.float32)
+    loss, grad, acc = model.compute_backprop(x32, y32)
+    params = [torch.tensor(p.astype(np.float64), requires_grad=True) for p in model.unflatten()]
+    w1, b1, w2, b2 = params
+    x, y = torch.tensor(x32, dtype=torch.float64), torch.tensor(y32, dtype=torch.float64)
+    prob = torch.softmax(torch.relu(x @ w1 + b1) @ w2 + b2, dim=1)
+    per_sample = -(torch.log(prob + 1e-16) * y).sum(dim=1)
+    per_sample.sum().backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in params]).numpy()
+    assert abs(loss - per_sample.mean().item()) <= 1e-6 * abs(loss)
+    scale = np.abs(ref).max()
+    assert np.abs(grad - ref).max() <= 1e-5 * scale
+    assert acc == (prob.argmax(1) == y.argmax(1)).double().mean().item()
+
+
+@pytest.mark.parametrize('seed', [5, 6])
+def test_mlp_rollout_fixture_regenerates(seed):
+    from oracle.gen_golden import mlp_dataset, rollout_mlp
+    data = golden('mlp_data_128x16.npz')
+    features, targets = mlp_dataset()
+    assert np.array_equal(features, data['features']) and np.array_equal(targets, data['targets'])
+    fx = golden('optimize_mlp_s%d.npz' % seed)
+    rec = rollout_mlp(features, targets, seed, action_seed=int(fx['action_seed']))
+    for key in ('reward', 'done', 'objective', 'accuracy', 'ep_len', 'loss_obs', 'obs',
+                'weights', 'reset_obs', 'init_weights'):
+        assert np.array_equal(rec[key], fx[key]), key
