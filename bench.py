@@ -16,7 +16,9 @@ custom_envs_amd/distributed.py), reported as its own line.
 
 ``--workload multi`` measures config 5 instead: MultiOptLRs-v0 (4 agents,
 4-D Rosenbrock pairs, H=5, max_batches=400) behind OptVecEnv, 1024 envs per
-GPU, actions uniform(1, 3) as in SURVEY 8d.
+GPU, actions uniform(1, 3) as in SURVEY 8d.  ``--workload mlp`` measures
+config 3: Optimize-v0 over the 784 -> 64 -> 10 MLP on 1024 MNIST-sized
+synthetic rows, B = 32, 4096 envs, float32 on MFMA (roofline bound "mfma").
 
 Rank 0 prints ONE JSON line.  With N>1 run under
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
@@ -36,6 +38,9 @@ sys.path.insert(0, ROOT)
 METRIC = 'vectorised env-steps/sec, Optimize-v0 @4096 envs, 1/2/4/8 MI355X vs host CPU'
 METRIC_MULTI = ('vectorised env-steps/sec, MultiOptLRs-v0 (4 agents) via OptVecEnv, '
                 'config 5, MI355X vs host CPU')
+METRIC_MLP = ('vectorised env-steps/sec, Optimize-v0 over the 784-64-10 MLP @4096 envs, '
+              'config 3, MI355X vs host CPU')
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 F64_VALU_PEAK_TFLOPS = 78.6
 
@@ -64,6 +69,20 @@ def multi_bytes_per_env_step(P, H, raw=5):
             + H * (8 + 16 * P) + 8 + 12 * H * P + 4 * P + P + 56 + 4)
 
 
+def mlp_flops(F=784, H=64, K=10, B=32, N=1024):
+    """Algorithmic FLOPs of one config-3 env-step: minibatch forward
+    2B(FH + HK), backward 2BFH + 4BHK, full-data info forward 2N(FH + HK)."""
+    train = 2 * B * (F * H + H * K) + 2 * B * F * H + 4 * B * H * K
+    info = 2 * N * (F * H + H * K)
+    return train, info
+
+
+def mlp_train_bytes(P):
+    """HBM bytes of the train kernel per env-step: action 4P, W r/w 8P, G (float64)
+    r/w 16P, obs 4(2P+1), L r/w 16, step r/w 8, reward/done/length 9."""
+    return 4 * P + 8 * P + 16 * P + 4 * (2 * P + 1) + 16 + 8 + 9
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
@@ -71,7 +90,7 @@ def parse():
     p.add_argument('--warmup', type=int, default=200)
     p.add_argument('--envs', type=int, default=None,
                    help='envs per GPU (default 4096 optimize, 1024 multi)')
-    p.add_argument('--workload', default='optimize', choices=['optimize', 'multi'])
+    p.add_argument('--workload', default='optimize', choices=['optimize', 'multi', 'mlp'])
     p.add_argument('--precision', default='f64', choices=['f64', 'f32'])
     p.add_argument('--graph-steps', type=int, default=250, help='steps per hipGraph replay')
     p.add_argument('--gather', action='store_true', help='all-gather outputs every step')
@@ -81,7 +100,7 @@ def parse():
                    help='run the timed steps only (for rocprofv3)')
     args = p.parse_args()
     if args.envs is None:
-        args.envs = 4096 if args.workload == 'optimize' else 1024
+        args.envs = 1024 if args.workload == 'multi' else 4096
     return args
 
 
@@ -169,6 +188,56 @@ def build_optimize(args, torch, device, rank, world):
     return eng, actions, S
 
 
+def mlp_dataset():
+    from custom_envs_amd.data import load_data
+    seq = load_data('mnist_synthetic', batch_size=32)
+    return seq.features, seq.targets
+
+
+def build_mlp(args, torch, device, rank, world, phases=None):
+    from custom_envs_amd.engine import OptimizeEngine
+    features, targets = mlp_dataset()
+    E = args.envs
+    if phases:
+        os.environ['CE_MLP_PHASES'] = phases
+    try:
+        eng = OptimizeEngine(features, targets, num_envs=E, batch_size=32, model='mlp',
+                             device=device)
+    finally:
+        os.environ.pop('CE_MLP_PHASES', None)
+    eng.seed([rank * E + i for i in range(E)])
+    gen = torch.Generator(device='cuda').manual_seed(4321 + rank)
+    S = 2                                  # two action blocks of [E][P] (833 MB each)
+    actions = torch.randn((S, E, eng.act_dim), generator=gen, device='cuda') * 1e-3
+    return eng, actions, S
+
+
+def cpu_baseline_mlp(envs, budget_s):
+    """Oracle float32 MLP Optimize envs under the restated ThreadVecEnv."""
+    from oracle.optimize import Optimize as OracleEnv
+    from oracle.vectorize import ThreadVecEnv
+    features, targets = mlp_dataset()
+    n = min(_raise_fd_limit(envs), 64)
+
+    def factory(seed):
+        def make():
+            env = OracleEnv(features, targets, batch_size=32, model='mlp')
+            env.seed(seed)
+            return env
+        return make
+
+    venv = ThreadVecEnv([factory(i) for i in range(n)])
+    venv.reset()
+    acts = np.random.RandomState(0).normal(0, 1e-3, (n, 50890)).astype(np.float32)
+    steps, wall, cpu = _time_cpu(venv, acts, budget_s)
+    venv.close()
+    return {'value': n * steps / wall, 'unit': 'env-steps/s',
+            'cores': max(1, int(round(cpu / wall))), 'kind': 'port',
+            'sample': '%d envs x %d steps of ThreadVecEnv over the numpy oracle Optimize env '
+                      'with the float32 784-64-10 MLP (BLAS sgemm); %.1f s wall, %.1f s CPU; '
+                      'os.cpu_count()=%d' % (n, steps, wall, cpu, os.cpu_count())}
+
+
 def build_multi(args, torch, device, rank, world):
     from custom_envs_amd.multi_engine import MultiOptEngine
     E = args.envs
@@ -194,9 +263,9 @@ def main():
         torch.cuda.set_device(0)
     device = torch.cuda.current_device()
     multi = args.workload == 'multi'
-
-    eng, actions, S = (build_multi if multi else build_optimize)(args, torch, device, rank,
-                                                                 world)
+    mlp = args.workload == 'mlp'
+    builder = {'optimize': build_optimize, 'multi': build_multi, 'mlp': build_mlp}[args.workload]
+    eng, actions, S = builder(args, torch, device, rank, world)
     E = args.envs
     stream = torch.cuda.Stream()          # a real stream: graphs cannot capture the null stream
     torch.cuda.set_stream(stream)
@@ -256,18 +325,47 @@ def main():
     torch.cuda.synchronize()
     times = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     kernel_ms, kernel_ms_mean = float(np.median(times)), float(np.mean(times))
+    phase_ms = {}
+    if mlp and rank == 0:
+        # each MLP kernel alone (CE_MLP_PHASES engines), same events method
+        for phase in ('train', 'info'):
+            peng, pact, _ = build_mlp(args, torch, device, rank, world, phases=phase)
+            peng.set_stream(stream.cuda_stream)
+            pout = peng.alloc_device_outputs()
+            peng.reset_device(pout)
+            for i in range(3):
+                peng.step_device(pact[i % 2], pout)
+            n_ph = 20
+            st = [torch.cuda.Event(enable_timing=True) for _ in range(n_ph)]
+            en = [torch.cuda.Event(enable_timing=True) for _ in range(n_ph)]
+            for i in range(n_ph):
+                st[i].record(stream)
+                peng.step_device(pact[i % 2], pout)
+                en[i].record(stream)
+            torch.cuda.synchronize()
+            phase_ms[phase] = float(np.median([a.elapsed_time(b) for a, b in zip(st, en)]))
+            peng.close()
+            del pact, pout
 
     host_rate = None
-    if rank == 0 and world == 1 and not multi:
+    if rank == 0 and world == 1 and args.workload == 'optimize':
         host_rate = host_loop_rate(args, device, E)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = (cpu_baseline_multi(E, args.cpu_seconds) if multi else
-               cpu_baseline(*lr_dataset(), E, args.cpu_seconds))
+        if multi:
+            cpu = cpu_baseline_multi(E, args.cpu_seconds)
+        elif mlp:
+            cpu = cpu_baseline_mlp(E, args.cpu_seconds)
+        else:
+            cpu = cpu_baseline(*lr_dataset(), E, args.cpu_seconds)
 
     if rank == 0:
-        line = (multi_line if multi else optimize_line)(args, eng, world, E, S, elapsed,
-                                                        kernel_ms, kernel_ms_mean, shard)
+        if mlp:
+            line = mlp_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard,
+                            phase_ms)
+        else:
+            line = (multi_line if multi else optimize_line)(args, eng, world, E, S, elapsed,
+                                                            kernel_ms, kernel_ms_mean, shard)
         line['cpu_baseline'] = cpu
         if host_rate is not None:
             line['host_loop_env_steps_per_s'] = host_rate
@@ -389,6 +487,43 @@ def multi_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard
             'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
             'kernel_ms_mean': kernel_ms_mean,
             'kernel': 'ce::multi_step_kernel<4>',
+        },
+    })
+    return line
+
+
+def mlp_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard, phase_ms):
+    P = eng.act_dim
+    train_f, info_f = mlp_flops()
+    info_ms = phase_ms.get('info') or kernel_ms
+    train_ms = phase_ms.get('train')
+    achieved = info_f * E / (info_ms * 1e-3) / 1e12
+    line = {'metric': METRIC_MLP}
+    line.update(_common(args, world, E, S, elapsed, shard))
+    line.update({
+        'dtype': 'f32',
+        'data': 'synthetic: RandomState(0).rand(1024, 784), labels argmax(X T), '
+                'T = RandomState(1).normal(784, 10); glorot-uniform init per env seed; '
+                'actions N(0, 1e-3) float32 generated on device',
+        'config': {
+            'workload': 'Optimize-v0 over the 784-64-10 relu MLP (P=50890, obs 101781), '
+                        '%d envs per GPU, B=32 of N=1024, full-data info pass every step, '
+                        'in-kernel auto-reset, device-resident actions/outputs' % E,
+            'envs_per_gpu': E, 'global_envs': world * E, 'n_rows': 1024, 'n_features': 784,
+            'n_hidden': 64, 'n_classes': 10, 'batch_size': 32,
+            'parallelism': 'env-sharded x%d (no collective)' % world,
+        },
+        'roofline': {
+            'bound': 'mfma', 'achieved': achieved, 'peak': MFMA_F32_PEAK_TFLOPS,
+            'unit': 'TFLOP/s', 'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': None,
+            'kernel': 'ce::mlp_info_kernel (full-data forward, 94% of the FLOPs)',
+            'flops_per_env_step': train_f + info_f, 'info_flops_per_env_step': info_f,
+            'info_kernel_ms': info_ms, 'train_kernel_ms': train_ms,
+            'step_ms_median': kernel_ms, 'step_ms_mean': kernel_ms_mean,
+            'step_tflops': (train_f + info_f) * E / (kernel_ms * 1e-3) / 1e12,
+            'train_kernel_hbm_bytes_per_env_step': mlp_train_bytes(P),
+            'train_kernel_gbs': (mlp_train_bytes(P) * E / (train_ms * 1e-3) / 1e9
+                                 if train_ms else None),
         },
     })
     return line

@@ -74,6 +74,7 @@ struct ce_engine {
     ce_config cfg{};
     int P = 0, obs_dim = 0;
     bool mlp = false;  // CE_PROBLEM_MLP
+    int mlp_phases = 3;  // bit 0: train kernel, bit 1: info kernel (CE_MLP_PHASES, profiling)
     size_t tsize = 8;  // element size of W / W0
     size_t gsize = 8;  // element size of G (grad_hist)
     const KernelEntry *kern = nullptr;
@@ -81,6 +82,7 @@ struct ce_engine {
     hipStream_t stream = nullptr;
     // device state
     void *X = nullptr;
+    float *Xs = nullptr;   // MLP: dataset in MFMA operand order (mlp_kernels.h)
     int32_t *label = nullptr;
     void *W = nullptr, *G = nullptr, *W0 = nullptr;
     double *L = nullptr;
@@ -161,6 +163,7 @@ ce::MlpArgs make_mlp_args(const ce_engine *e, const float *act, const ce_outputs
     a.max_steps = e->cfg.max_steps;
     a.auto_reset = e->cfg.auto_reset;
     a.X = static_cast<const float *>(e->X);
+    a.Xs = e->Xs;
     a.label = e->label;
     a.W = static_cast<float *>(e->W);
     a.W0 = static_cast<const float *>(e->W0);
@@ -188,8 +191,8 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
         if (reset) {
             hipLaunchKernelGGL(ce::mlp_reset_kernel, grid, block, 0, stream, a);
         } else {
-            hipLaunchKernelGGL(ce::mlp_train_kernel, grid, block, 0, stream, a);
-            hipLaunchKernelGGL(ce::mlp_info_kernel, grid, block, 0, stream, a);
+            if (e->mlp_phases & 1) hipLaunchKernelGGL(ce::mlp_train_kernel, grid, block, 0, stream, a);
+            if (e->mlp_phases & 2) hipLaunchKernelGGL(ce::mlp_info_kernel, grid, block, 0, stream, a);
         }
         return;
     }
@@ -340,6 +343,11 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     e->cfg = *cfg;
     e->kern = kern;
     e->mlp = mlp;
+    // experiment switch: launch one phase only, to time each kernel alone
+    if (const char *ph = std::getenv("CE_MLP_PHASES")) {
+        if (std::strcmp(ph, "train") == 0) e->mlp_phases = 1;
+        if (std::strcmp(ph, "info") == 0) e->mlp_phases = 2;
+    }
     if (mlp) {
         const int F = cfg->n_features, H = cfg->n_hidden, K = cfg->n_classes;
         e->P = F * H + H + H * K + K;
@@ -370,6 +378,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     const size_t E = cfg->num_envs, N = cfg->n_rows, F = cfg->n_features, P = e->P;
     if (mlp) {
         CE_TRY(hipMalloc(&e->X, N * F * sizeof(float)));
+        CE_TRY(hipMalloc(&e->Xs, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
     } else {
         CE_TRY(hipMalloc(&e->X, ce::stage_bytes_total(cfg->n_features, cfg->n_rows,
@@ -415,6 +424,15 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         std::vector<float> x32(N * F);
         for (size_t i = 0; i < N * F; ++i) x32[i] = static_cast<float>(features[i]);
         CE_TRY(hipMemcpy(e->X, x32.data(), N * F * sizeof(float), hipMemcpyHostToDevice));
+        std::vector<float> xs(N * F);
+        const size_t chunks = F / 8;
+        for (size_t t = 0; t < N / 32; ++t)
+            for (size_t c = 0; c < chunks; ++c)
+                for (size_t l = 0; l < 64; ++l)
+                    for (size_t j = 0; j < 4; ++j)
+                        xs[((t * chunks + c) * 64 + l) * 4 + j] =
+                            x32[(32 * t + (l & 31)) * F + 8 * c + 4 * (l >> 5) + j];
+        CE_TRY(hipMemcpy(e->Xs, xs.data(), N * F * sizeof(float), hipMemcpyHostToDevice));
         CE_TRY(hipMemcpy(e->label, labels, N * sizeof(int32_t), hipMemcpyHostToDevice));
     }
 #undef CE_TRY
@@ -457,7 +475,7 @@ void ce_destroy(ce_engine *e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->graph) (void)hipGraphExecDestroy(e->graph);
-    void *dev[] = {e->X, e->label, e->W, e->G, e->W0, e->L, e->step,
+    void *dev[] = {e->X, e->Xs, e->label, e->W, e->G, e->W0, e->L, e->step,
                    e->perm, e->order, e->order_sel, e->d_act, e->d_out, e->diag};
     for (void *p : dev)
         if (p) (void)hipFree(p);

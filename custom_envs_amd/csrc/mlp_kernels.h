@@ -1,7 +1,8 @@
 // Optimize-v0 over the config-3 MLP problem for gfx950.
 //
-// One VecEnv.step of E envs is two launches on one stream:
-//   mlp_train_kernel  one 256-thread workgroup per env:
+// One VecEnv.step of E envs is two launches on one stream, each a 256-thread
+// workgroup per env:
+//   mlp_train_kernel:
 //     Optimize.base_step        custom_envs/envs/optimize.py:69-93
 //       W <- W - a              (:74-75), fused into the forward's operand loads
 //       minibatch forward/backward of the F -> 64 (relu) -> K softmax MLP
@@ -9,7 +10,7 @@
 //       flat parameter order [W1 | b1 | W2 | b2] (utils_common.py:199-207)
 //       g / B, L' = (loss - L)/(L + 0.1), G' = g/(|G| + 1)   (:78-83)
 //       obs = [0 (P) | L' | G' (P)], reward = -loss, done = step >= 40
-//   mlp_info_kernel  one workgroup per env:
+//   mlp_info_kernel:
 //       info objective/accuracy over the full dataset     (optimize.py:94-97)
 //       auto-reset of finished envs (utils_venv.py:31): W <- W0, histories 0,
 //       row order composed with the reset permutation (inmemorydataset
@@ -38,12 +39,16 @@ constexpr int kMlpHidden = 64;
 constexpr int kMlpBatch = 32;
 constexpr int kMlpMaxK = 16;
 constexpr int kMlpBlock = 256;   // 4 waves
+constexpr int kInfoTiles = 8;    // 32-sample tiles per wave per info pass
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 struct MlpArgs {
     int E, N, F, K, P, max_steps, auto_reset;
     const float *X;          // [N][F] dataset rows (dataset order)
+    const float *Xs;         // the same rows in MFMA operand order:
+                             // [N/32 tiles][F/8 chunks][64 lanes][4], element j of
+                             // lane l = X[32 t + (l & 31)][8 c + 4 (l >> 5) + j]
     const int32_t *label;    // [N]
     float *W;                // [E][P]
     const float *W0;         // [E][P]
@@ -84,7 +89,7 @@ __device__ __forceinline__ void write_grad(const MlpArgs &a, size_t e, int idx, 
     a.obs[e * (2 * static_cast<size_t>(a.P) + 1) + a.P + 1 + idx] = static_cast<float>(gn);
 }
 
-__global__ __launch_bounds__(kMlpBlock) void mlp_train_kernel(MlpArgs a) {
+__device__ __forceinline__ void mlp_train_body(const MlpArgs &a, const size_t e) {
     __shared__ float part[4][kMlpHidden][kMlpBatch];     // per-wave partial H^T
     __shared__ float hs[kMlpBatch][kMlpHidden + 1];      // H, then dz1 (sample-major)
     __shared__ float w2s[kMlpHidden][kMlpMaxK];
@@ -95,7 +100,6 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_train_kernel(MlpArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, h = lane >> 5;
-    const size_t e = blockIdx.x;
     const int F = a.F, K = a.K, P = a.P;
     int ob1, oW2, ob2;
     mlp_offsets(a, ob1, oW2, ob2);
@@ -126,18 +130,40 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_train_kernel(MlpArgs a) {
         const int c0 = wave * chunks / 4, c1 = (wave + 1) * chunks / 4;
         f32x16 acc0 = {}, acc1 = {};
         const float *xrow = a.X + static_cast<size_t>(rows[li]) * F + 4 * h;
+        // operands of chunk c + 1 are loaded while chunk c is on the MFMA pipe
+        float4 xn = *reinterpret_cast<const float4 *>(xrow + 8 * c0);
+        float wn[8], an[8];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int base = (8 * c0 + 4 * h + jj) * kMlpHidden + li;
+            wn[2 * jj] = W[base];
+            wn[2 * jj + 1] = W[base + 32];
+            an[2 * jj] = act[base];
+            an[2 * jj + 1] = act[base + 32];
+        }
         for (int c = c0; c < c1; ++c) {
-            const float4 xv = *reinterpret_cast<const float4 *>(xrow + 8 * c);
-            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+            const float xs[4] = {xn.x, xn.y, xn.z, xn.w};
+            float wc[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) wc[q] = wn[q] - an[q];
+            if (c + 1 < c1) {
+                xn = *reinterpret_cast<const float4 *>(xrow + 8 * (c + 1));
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int base = (8 * (c + 1) + 4 * h + jj) * kMlpHidden + li;
+                    wn[2 * jj] = W[base];
+                    wn[2 * jj + 1] = W[base + 32];
+                    an[2 * jj] = act[base];
+                    an[2 * jj + 1] = act[base + 32];
+                }
+            }
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
                 const int base = (8 * c + 4 * h + jj) * kMlpHidden + li;
-                const float w0 = W[base] - act[base];
-                const float w1 = W[base + 32] - act[base + 32];
-                W[base] = w0;
-                W[base + 32] = w1;
-                acc0 = mfma32(w0, xs[jj], acc0);
-                acc1 = mfma32(w1, xs[jj], acc1);
+                W[base] = wc[2 * jj];
+                W[base + 32] = wc[2 * jj + 1];
+                acc0 = mfma32(wc[2 * jj], xs[jj], acc0);
+                acc1 = mfma32(wc[2 * jj + 1], xs[jj], acc1);
             }
         }
 #pragma unroll
@@ -214,24 +240,28 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_train_kernel(MlpArgs a) {
         write_grad(a, e, ob1 + tid, acc * inv_b);
     }
 
-    // ---- dW1 = X_b^T dz1 on MFMA: 32 features x 32 hidden per tile, K = 32
+    // ---- dW1 = X_b^T dz1 on MFMA: 32 features x 64 hidden per tile (two
+    // accumulators sharing the X operand), K = 32 samples; G' and obs from the
+    // accumulators, each feature row's 64 values written as one 512-B run
     {
         const int ftiles = (F + 31) / 32;
-        for (int t = wave; t < 2 * ftiles; t += 4) {
-            const int ft = t >> 1, ht = t & 1;
+        for (int ft = wave; ft < ftiles; ft += 4) {
             const int f = ft * 32 + li;
-            f32x16 acc = {};
+            f32x16 acc0 = {}, acc1 = {};
 #pragma unroll 4
             for (int ks = 0; ks < kMlpBatch / 2; ++ks) {
                 const int s = 2 * ks + h;
                 const float xa = f < F ? a.X[static_cast<size_t>(rows[s]) * F + f] : 0.0f;
-                acc = mfma32(xa, hs[s][ht * 32 + li], acc);
+                acc0 = mfma32(xa, hs[s][li], acc0);
+                acc1 = mfma32(xa, hs[s][32 + li], acc1);
             }
-            const int hid = ht * 32 + li;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int fr = ft * 32 + acc_row(r, h);
-                if (fr < F) write_grad(a, e, fr * kMlpHidden + hid, acc[r] * inv_b);
+                if (fr < F) {
+                    write_grad(a, e, fr * kMlpHidden + li, acc0[r] * inv_b);
+                    write_grad(a, e, fr * kMlpHidden + 32 + li, acc1[r] * inv_b);
+                }
             }
         }
     }
@@ -284,7 +314,7 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_reset_kernel(MlpArgs a) {
 
 // Full-dataset forward for info['objective'] / info['accuracy'] with the
 // updated weights, then the auto-reset of envs that just finished.
-__global__ __launch_bounds__(kMlpBlock) void mlp_info_kernel(MlpArgs a) {
+__device__ __forceinline__ void mlp_info_body(const MlpArgs &a, const size_t e) {
     __shared__ float w2s[kMlpHidden][kMlpMaxK];
     __shared__ float b1s[kMlpHidden], b2s[kMlpMaxK];
     __shared__ float red_loss[4];
@@ -292,7 +322,6 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_info_kernel(MlpArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, h = lane >> 5;
-    const size_t e = blockIdx.x;
     const int F = a.F, K = a.K, P = a.P;
     int ob1, oW2, ob2;
     mlp_offsets(a, ob1, oW2, ob2);
@@ -309,27 +338,63 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_info_kernel(MlpArgs a) {
     float loss_acc = 0.0f;
     int hits = 0;
     const int tiles = a.N / 32;
-    for (int st = wave * 2; st < tiles; st += 8) {     // two sample tiles per pass
-        f32x16 acc[2][2] = {};
-        const float *x0 = a.X + static_cast<size_t>(st * 32 + li) * F + 4 * h;
-        const float *x1 = x0 + static_cast<size_t>(32) * F;
-        for (int c = 0; c < F / 8; ++c) {
-            const float4 xa = *reinterpret_cast<const float4 *>(x0 + 8 * c);
-            const float4 xb = *reinterpret_cast<const float4 *>(x1 + 8 * c);
-            const float xs0[4] = {xa.x, xa.y, xa.z, xa.w};
-            const float xs1[4] = {xb.x, xb.y, xb.z, xb.w};
+    const int chunks = F / 8;
+    const size_t tstride = static_cast<size_t>(chunks) * 64 * 4;   // floats per swizzled tile
+    // A pass gives each wave kInfoTiles consecutive 32-sample tiles: 2 x kInfoTiles
+    // accumulators live across one sweep over K, so every W1 fragment a wave
+    // loads feeds 2 kInfoTiles MFMAs and W1 is read once per wave per pass.
+    for (int t0 = wave * kInfoTiles; t0 < tiles; t0 += 4 * kInfoTiles) {
+        const int nt = tiles - t0 < kInfoTiles ? tiles - t0 : kInfoTiles;   // wave-uniform
+        f32x16 acc[kInfoTiles][2];
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const int base = (8 * c + 4 * h + jj) * kMlpHidden + li;
-                const float w0 = W[base], w1 = W[base + 32];
-                acc[0][0] = mfma32(w0, xs0[jj], acc[0][0]);
-                acc[0][1] = mfma32(w1, xs0[jj], acc[0][1]);
-                acc[1][0] = mfma32(w0, xs1[jj], acc[1][0]);
-                acc[1][1] = mfma32(w1, xs1[jj], acc[1][1]);
+        for (int q = 0; q < kInfoTiles; ++q) acc[q][0] = acc[q][1] = f32x16{};
+        const float *xb = a.Xs + (static_cast<size_t>(t0) * chunks * 64 + lane) * 4;
+        // operands of chunk c + 1 are loaded while chunk c is on the MFMA pipe
+        float4 xn[kInfoTiles];
+        float wn[8];
+        // tiles past the end of a partial pass read tile 0 (valid memory); their
+        // accumulators are never used, so the MFMA loop stays branch-free
+        size_t toff[kInfoTiles];
+#pragma unroll
+        for (int q = 0; q < kInfoTiles; ++q) {
+            toff[q] = (q < nt ? q : 0) * tstride;
+            xn[q] = *reinterpret_cast<const float4 *>(xb + toff[q]);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int base = (4 * h + jj) * kMlpHidden + li;
+            wn[2 * jj] = W[base];
+            wn[2 * jj + 1] = W[base + 32];
+        }
+        for (int c = 0; c < chunks; ++c) {
+            float wc[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) wc[q] = wn[q];
+            if (c + 1 < chunks) {
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int base = (8 * (c + 1) + 4 * h + jj) * kMlpHidden + li;
+                    wn[2 * jj] = W[base];
+                    wn[2 * jj + 1] = W[base + 32];
+                }
+            }
+            // tile-major: tile q's X register is reloaded for chunk c + 1 as
+            // soon as its 8 MFMAs of chunk c have issued
+#pragma unroll
+            for (int q = 0; q < kInfoTiles; ++q) {
+                const float xs[4] = {xn[q].x, xn[q].y, xn[q].z, xn[q].w};
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    acc[q][0] = mfma32(wc[2 * jj], xs[jj], acc[q][0]);
+                    acc[q][1] = mfma32(wc[2 * jj + 1], xs[jj], acc[q][1]);
+                }
+                if (c + 1 < chunks)
+                    xn[q] = *reinterpret_cast<const float4 *>(xb + toff[q] + 256 * (c + 1));
             }
         }
 #pragma unroll
-        for (int ts = 0; ts < 2; ++ts) {
+        for (int q = 0; q < kInfoTiles; ++q) {
+            if (q >= nt) continue;
             // bias + relu on H^T, then logits^T = W2^T H^T with H^T as the B operand
             f32x16 lg = {};
 #pragma unroll
@@ -337,7 +402,7 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_info_kernel(MlpArgs a) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int hid = ht * 32 + acc_row(r, h);
-                    const float z = acc[ts][ht][r] + b1s[hid];
+                    const float z = acc[q][ht][r] + b1s[hid];
                     const float hv = z > 0.0f ? z : 0.0f;
                     const float wa = li < K ? w2s[hid][li] : 0.0f;
                     lg = mfma32(wa, hv, lg);
@@ -355,10 +420,9 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_info_kernel(MlpArgs a) {
                     m = fmaxf(m, z);
                 }
             }
-            const float mo = __shfl_xor(m, 32);
-            m = fmaxf(m, mo);
+            m = fmaxf(m, __shfl_xor(m, 32));
             float sum = 0.0f;
-            const int row = st * 32 + ts * 32 + li;
+            const int row = (t0 + q) * 32 + li;
             const int y = a.label[row];
             float zy = 0.0f;
 #pragma unroll
@@ -404,6 +468,17 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_info_kernel(MlpArgs a) {
     const bool wipe = a.auto_reset && a.step[e] >= a.max_steps;
     __syncthreads();
     if (wipe) mlp_reset_env(a, e, true);
+}
+
+// The two phases of a step, launched back to back on one stream.  The train
+// phase streams state (HBM-bound) at 2 waves per SIMD; the info phase holds
+// 16 32x32 accumulators per wave (one wave per SIMD, 512 registers).
+__global__ __launch_bounds__(kMlpBlock) void mlp_train_kernel(MlpArgs a) {
+    mlp_train_body(a, blockIdx.x);
+}
+
+__global__ __launch_bounds__(kMlpBlock) void mlp_info_kernel(MlpArgs a) {
+    mlp_info_body(a, blockIdx.x);
 }
 
 }  // namespace ce
