@@ -9,8 +9,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd.so')
 # CE_LIB=diag selects the phase-stamped profiling build (same ABI + ce_diag_stamps)
+# CE_LIB=<name> selects lib/libcustom_envs_amd_<name>.so (experiment builds).
 if os.environ.get('CE_LIB') == 'diag':
     LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd_diag.so')
+elif os.environ.get('CE_LIB'):
+    LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd_%s.so' % os.environ['CE_LIB'])
 
 ABI_VERSION = 2
 CE_OK, CE_EINVAL, CE_EHIP, CE_ENOMEM, CE_ESTATE, CE_EUNSUPPORTED = 0, -1, -2, -3, -4, -5

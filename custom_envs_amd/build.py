@@ -33,7 +33,7 @@ def sources():
 
 def headers():
     return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'multiopt_kernels.h',
-                                            'common.h', 'seeding.h')] + [
+                                            'mlp_kernels.h', 'common.h', 'seeding.h')] + [
         os.path.join(ROOT, 'include', 'custom_envs_amd.h')]
 
 
@@ -49,16 +49,24 @@ def up_to_date(diag=False):
     return all(os.path.getmtime(p) <= mtime for p in sources() + headers())
 
 
-def build(force=False, verbose=False, diag=False):
+def build(force=False, verbose=False, diag=False, variant=None, defines=()):
+    """Build the engine; `variant` + `defines` make an experiment build
+    lib/libcustom_envs_amd_<variant>.so (selected at run time by CE_LIB)."""
+    if variant:
+        out = os.path.join(LIBDIR, 'libcustom_envs_amd_%s.so' % variant)
+        return _compile(out, os.path.join(LIBDIR, 'obj_' + variant), list(defines), verbose)
     if not force and up_to_date(diag):
         return lib_path(diag)
+    return _compile(lib_path(diag), os.path.join(LIBDIR, 'obj_diag' if diag else 'obj'),
+                    ['CE_DIAG'] if diag else [], verbose)
+
+
+def _compile(out, tmp, defines, verbose):
     os.makedirs(LIBDIR, exist_ok=True)
     hipcc = _hipcc()
     objs = []
     common = ['-O3', '-fPIC', '-std=c++17', '-Wall', '-I', os.path.join(ROOT, 'include')]
-    if diag:
-        common.append('-DCE_DIAG')
-    tmp = os.path.join(LIBDIR, 'obj_diag' if diag else 'obj')
+    common += ['-D' + d for d in defines]
     os.makedirs(tmp, exist_ok=True)
     for src in sources():
         obj = os.path.join(tmp, os.path.basename(src) + '.o')
@@ -70,7 +78,6 @@ def build(force=False, verbose=False, diag=False):
             print(' '.join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    out = lib_path(diag)
     cmd = [hipcc, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out + '.tmp'] + objs
     subprocess.run(cmd, check=True)
     os.replace(out + '.tmp', out)

@@ -438,13 +438,18 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
 #undef CE_TRY
     if (!mlp) {
     // [rows | labels]: row-major rows padded to ce::row_stride elements (zeros
-    // in the pad), then the int32 labels, in one buffer staged with one copy
+    // in the pad), then the int32 labels, in one buffer staged with one copy.
+    // Two-class shapes store s_y x with s_y = +1 (y = 0) / -1 (y = 1)
+    // (ce::signed_rows, optimize_kernels.h): exact, and it folds the label
+    // into the row's dot product.
     const size_t RS = ce::row_stride(cfg->n_features, static_cast<int>(e->tsize));
     const size_t xbytes = ce::align16(N * RS * e->tsize);
+    const bool sign_fold = ce::signed_rows(cfg->n_features, cfg->n_classes);
     std::vector<unsigned char> blob(ce::align16(xbytes + 4 * N), 0);
     for (size_t r = 0; r < N; ++r)
         for (size_t f = 0; f < F; ++f) {
-            const double v = features[r * F + f];
+            const double v = (sign_fold && labels[r] != 0) ? -features[r * F + f]
+                                                           : features[r * F + f];
             if (cfg->precision == CE_F64) {
                 std::memcpy(&blob[(r * RS + f) * 8], &v, 8);
             } else {

@@ -44,26 +44,22 @@
 
 namespace ce {
 
+
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 16;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr size_t kStageLimit = 64 * 1024;   // LDS bytes a block may stage
 
-// Near-minimax (Chebyshev-fitted) polynomials for the two-class fast path:
+// Near-minimax (Chebyshev-fitted) polynomial for the two-class fast path:
 //   exp(r),  |r| <= ln2/2 : degree 10, rel. err 6.7e-16 (c0 = 1 exactly, so
 //                           exp(0) == 1 as in libm)
-//   atanh(s)/s = g(s^2), s^2 <= 0.02944 : degree 6 in s^2, rel. err 4.4e-16
-// (fits: scripts/fit_poly.py).  Horner order is from the top coefficient.
+// (fit: scripts/fit_poly.py).  Horner order is from the top coefficient.
 constexpr int kExpTerms = 11;
-constexpr int kLogTerms = 7;
 constexpr double kExpCoef[kExpTerms] = {
     1.0, 1.000000000000006, 0.49999999999997946, 0.16666666666560392,
     0.041666666667466275, 0.008333333384270189, 0.0013888888768614806,
     0.00019841171680137992, 2.4801650828121558e-05, 2.7639677785365415e-06,
     2.7575738554394086e-07};
-constexpr double kLogCoef[kLogTerms] = {
-    1.0, 0.33333333333278237, 0.20000000030151868, 0.14285708126945562,
-    0.11111708755950479, 0.09061251072084696, 0.08415323922275515};
 constexpr double kLn2Hi = 6.93147180369123816490e-01;
 constexpr double kLn2Lo = 1.90821492927058770002e-10;
 constexpr double kLog2e = 1.44269504088896338700e+00;
@@ -294,8 +290,11 @@ __device__ __forceinline__ T wave_sum(T v) { return lane_sum<T, 32>(v); }
 
 // ---------------------------------------------------------------------------
 // Problem kernels.  Each "Model" describes the per-row math, how many values
-// a lane accumulates (NE gradient elements + loss + hits), and how a reduced
-// element maps back to parameters.
+// a lane accumulates (NE gradient elements, then the loss and the hit count),
+// and how a reduced element maps back to parameters.  A row call adds the
+// row's gradient terms to g[0..NE), its loss term to `loss`, a factor to
+// `prod` (models with kProd: sum log(1 + t) is taken as log of a product)
+// and its argmax hit to `hits`.
 //
 // General K: the softmax classifier exactly as written in the reference.
 template <typename T, int F, int K>
@@ -303,17 +302,26 @@ struct SoftmaxModel {
     static constexpr int P = F * K;
     static constexpr int NE = P;           // reduced gradient elements
     static constexpr int NB = F * K;       // broadcast weight values
+    static constexpr bool kProd = false;
 
     static __device__ __forceinline__ void broadcast(T wl, T (&w)[NB]) {
 #pragma unroll
         for (int j = 0; j < NB; ++j) w[j] = readlane(wl, j);
     }
 
-    // Returns the row's loss term and hit; adds x^T (p - y) into acc if grad.
+    static constexpr bool kFixup = false;
+    struct Watch {
+        __device__ __forceinline__ bool flagged() const { return false; }
+    };
+    template <bool MASKED>
+    static __device__ __forceinline__ void fixup(const T (&)[F], const T (&)[NB],
+                                                 const int32_t *, int, bool, T &, int &) {}
+
     template <bool GRAD, bool MASKED, int NA>
-    static __device__ __forceinline__ void row(const T (&x)[F], const T (&w)[NB], int y,
-                                               bool valid, const MathConsts<T> &,
-                                               T (&acc)[NA], T &loss_term, T &hit) {
+    static __device__ __forceinline__ void row(const T (&x)[F], const T (&w)[NB],
+                                               const int32_t *ys, int r, bool valid,
+                                               T (&acc)[NA], T &loss, T &, int &hits, Watch &) {
+        const int y = ys[r];
         T logit[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -340,8 +348,8 @@ struct SoftmaxModel {
             if (k == y) py = p[k]; else rest += p[k];
         }
         valid = valid || !MASKED;
-        loss_term = valid ? -log_t(py + T(1e-16)) : T(0);
-        hit = (valid && best == y) ? T(1) : T(0);
+        loss += valid ? -log_t(py + T(1e-16)) : T(0);
+        hits += (valid && best == y) ? 1 : 0;
         if (GRAD) {
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -375,66 +383,68 @@ __device__ __forceinline__ double rcp_unit(double d) {
 __device__ __forceinline__ float rcp_unit(float d) { return __builtin_amdgcn_rcpf(d); }
 
 // exp(-a) for a >= 0:  n = rint(a log2e),  r = n ln2 - a in [-ln2/2, ln2/2],
-// exp(-a) = 2^-n exp(r).
+// exp(-a) = 2^-n exp(r).  a is clamped at 750, past which exp(-a) is 0 in
+// float64 (ldexp underflows), so huge |z| cannot push r out of range.
 template <typename T>
 __device__ __forceinline__ T exp_neg(T a, const MathConsts<T> &) {
+    a = fmin(a, T(750));
     const T n = rint(a * kLog2e);
     const T r = fma(n, kLn2Lo, fma(n, kLn2Hi, -a));
     T q = kExpCoef[kExpTerms - 1];
 #pragma unroll
     for (int k = kExpTerms - 2; k >= 0; --k) q = fma(q, r, kExpCoef[k]);
-    const T v = ldexp(q, -static_cast<int>(n));
-    return a < T(700) ? v : T(0);
+    return ldexp(q, -static_cast<int>(n));
 }
 
-// log(1 + t) for t in [0, 1]:  1 + t = 2^e m,
-// log1p(t) = e ln2 + 2 atanh(s), s = (m - 1)/(m + 1) in [-0.1716, 0.1716]:
-//   e = 0: s = t / (2 + t)          (keeps full relative accuracy as t -> 0)
-//   e = 1: s = (t - 1) / (t + 3)
-template <typename T>
-__device__ __forceinline__ T log1p_unit(T t, const MathConsts<T> &) {
-    const bool hi = t > T(0.41421356237309503);
-    const T s = (hi ? t - T(1) : t) * rcp_unit(hi ? t + T(3) : t + T(2));
-    const T s2 = s * s;
-    T q = kLogCoef[kLogTerms - 1];
-#pragma unroll
-    for (int k = kLogTerms - 2; k >= 0; --k) q = fma(q, s2, kLogCoef[k]);
-    return fma(T(2) * s, q, hi ? kLn2Lo : T(0)) + (hi ? kLn2Hi : T(0));
-}
-
-// float32 engine: hardware v_exp_f32 / v_log_f32 (about 1 ulp of float).
+// float32 engine: hardware v_exp_f32 (about 1 ulp of float).
 __device__ __forceinline__ float exp_neg(float a, const MathConsts<float> &) {
     return __expf(-a);
 }
-__device__ __forceinline__ float log1p_unit(float t, const MathConsts<float> &) {
-    return __logf(1.0f + t);
-}
 
-// -log(q) for any positive normal q, inline: q = 2^e m, m in [1, 2),
-// log(m) = log1p(m - 1) with m - 1 exact.  Used for the literal
-// -log(p + 1e-16) of rows whose minority-class probability is tiny.
-__device__ __forceinline__ double neg_log_eps(double p) {
-    const double q = p + 1e-16;
-    const int ex = __builtin_amdgcn_frexp_exp(q) - 1;   // q = 2^ex * m, m in [1, 2)
-    const double m = ldexp(__builtin_amdgcn_frexp_mant(q), 1);
-    const double lm = log1p_unit(m - 1.0, MathConsts<double>());
-    return -(fma(static_cast<double>(ex), kLn2Hi, fma(static_cast<double>(ex), kLn2Lo, lm)));
+// log(q) for any positive normal q, inline: q = 2^ex m, m in [1/2, 1).
+// y0 = log(m) from v_log_f32 (~1e-7 relative) is refined with the float64
+// exp already used by the row loop:  d = m exp(-y0) - 1 (|d| ~ 1e-7),
+// log(m) = y0 + log1p(d) = y0 + d - d^2/2 + d^3/3 (+ O(d^4) ~ 1e-28).
+// No logarithm coefficient table, so nothing beyond the exp constants has
+// to stay resident in registers across the row loop.
+__device__ __forceinline__ double log_pos(double q) {
+    const int ex = __builtin_amdgcn_frexp_exp(q);       // q = 2^ex * m, m in [1/2, 1)
+    const double m = __builtin_amdgcn_frexp_mant(q);
+    const double y0 = static_cast<double>(__logf(static_cast<float>(m)));
+    const double d = fma(m, exp_neg(y0, MathConsts<double>()), -1.0);
+    const double lm = fma(d * d, fma(d, 1.0 / 3.0, -0.5), d) + y0;
+    return fma(static_cast<double>(ex), kLn2Hi, fma(static_cast<double>(ex), kLn2Lo, lm));
 }
-__device__ __forceinline__ float neg_log_eps(float p) { return -__logf(p + 1e-16f); }
+__device__ __forceinline__ float log_pos(float q) { return __logf(q); }
 
-// K = 2: the same softmax in its two-class form (see file header).
-//   t = exp(-|z|), p_max = 1/(1+t), p_min = t/(1+t)
-//   -log(p_max + 1e-16) = log1p(t)            (p_max >= 1/2: the 1e-16 is
-//                                               below half an ulp of the log)
-//   -log(p_min + 1e-16) = |z| + log1p(t)      when p_min >= 1e-6 (dropping
-//                                               1e-16 moves it < 1e-10)
-//   otherwise the literal -log(p_min + 1e-16) (rare, data-dependent branch).
+// Two-class rows are stored pre-multiplied by s_y = +1 (y = 0) or -1 (y = 1)
+// (engine.hip builds the image), so one dot product gives u = s_y z with
+// z = x.(w0 - w1) the logit margin of class 0.  Negating an FMA chain's
+// inputs negates its result exactly, so |u| = |z| bit for bit.
+__host__ __device__ constexpr bool signed_rows(int F, int K) { return K == 2 && F + 2 <= 32; }
+
+// K = 2: the same softmax in its two-class form.  With t = exp(-|z|):
+//   p_max = 1/(1+t), p_min = t/(1+t)   (u < 0: y is the smaller-logit class)
+//   q     = 1 - p_y = (u < 0 ? p_max : p_min)   (probability of the other class)
+//   CE    = -log(p_y + 1e-16)                  (utils_math.py:25-34, literally)
+//   p_0 - y_0 = -s_y q, so x (p_0 - y_0) = -(s_y x) q: the gradient column 0
+//                        is minus the sum of x~ q, column 1 is plus it.
+//   argmax hit = u > 0, exact unless t == 1 (p_max == p_min, a tie: the
+//                        reference's np.argmax then picks class 0).
+// In float64 the row loop carries no logarithm: sum_i -log(p_y,i + 1e-16) is
+// taken as -log of the lane's product of the (p_y + 1e-16) factors, each in
+// (1e-16, 1], folded into the sum every kProdFold rows so it cannot
+// underflow.  The loop is branch-free; it tracks max(t) per lane, and rows
+// with t == 1 get the exact tie argmax from `fixup`, in a second pass a wave
+// takes only if one of its lanes saw a tie (practically never: |z| < 2^-53).
 template <typename T, int F>
 struct TwoClassModel {
     static constexpr int K = 2;
     static constexpr int P = F * 2;
     static constexpr int NE = F;           // column 1 of the gradient = -column 0
     static constexpr int NB = F;           // broadcast w0 - w1
+    static constexpr bool kProd = std::is_same<T, double>::value;
+    static constexpr bool kFixup = true;
 
     static __device__ __forceinline__ void broadcast(T wl, T (&wd)[NB]) {
         const T d = wl - __shfl_down(wl, 1);       // lane 2f: w[f][0] - w[f][1]
@@ -442,43 +452,63 @@ struct TwoClassModel {
         for (int f = 0; f < F; ++f) wd[f] = readlane(d, 2 * f);
     }
 
+    static __device__ __forceinline__ T margin(const T (&x)[F], const T (&wd)[NB]) {
+        T u = x[0] * wd[0];
+#pragma unroll
+        for (int f = 1; f < F; ++f) u = fma(x[f], wd[f], u);
+        return u;
+    }
+
+    // Per lane: tmax = max t over the lane's rows (t == 1 marks a tie).
+    struct Watch {
+        T tmax = T(0);
+        __device__ __forceinline__ bool flagged() const { return tmax == T(1); }
+    };
+
     template <bool GRAD, bool MASKED, int NA>
-    static __device__ __forceinline__ void row(const T (&x)[F], const T (&wd)[NB], int y,
-                                               bool valid, const MathConsts<T> &mc,
-                                               T (&acc)[NA], T &loss_term, T &hit) {
-        T z = x[0] * wd[0];
-#pragma unroll
-        for (int f = 1; f < F; ++f) z = fma(x[f], wd[f], z);
-        const T az = fabs(z);
-        const T t = exp_neg(az, mc);
-        const T inv = rcp_unit(T(1) + t);           // p of the larger-logit class
-        const T lo = t * inv;                       // p of the other class
-        const bool y0 = y == 0;
-        const bool y_is_min = y0 != (z >= T(0));   // class 0 wins ties (z = 0)
-        T lt = log1p_unit(t, mc) + (y_is_min ? az : T(0));
-        const bool tiny = y_is_min && lo < T(1e-6);
-        if (__any(tiny)) {                         // wave-uniform: skipped unless needed
-            if (tiny) lt = neg_log_eps(lo);
+    static __device__ __forceinline__ void row(const T (&x)[F], const T (&wd)[NB],
+                                               const int32_t *, int, bool valid,
+                                               T (&acc)[NA], T &loss, T &prod, int &hits,
+                                               Watch &wt) {
+        const T u = margin(x, wd);
+        const T t = exp_neg(fabs(u), MathConsts<T>());
+        const T inv = rcp_unit(T(1) + t);            // p of the larger-logit class
+        const T lo = t * inv;                        // p of the other class
+        const bool neg = u < T(0);
+        T q = neg ? inv : lo;
+        T py = (neg ? lo : inv) + T(1e-16);
+        bool hit = u > T(0);
+        if (MASKED && !valid) {
+            q = T(0);
+            py = T(1);
+            hit = false;
         }
-        // np.argmax(P) == y with first-maximum ties (p equal only if inv == lo)
-        const bool tie = !(inv > lo);
-        const bool hit_b = y0 ? (!y_is_min || tie) : (!y_is_min && !tie);
-        loss_term = MASKED && !valid ? T(0) : lt;
-        hit = (hit_b && (!MASKED || valid)) ? T(1) : T(0);
+        wt.tmax = fmax(wt.tmax, (MASKED && !valid) ? T(0) : t);
+        if constexpr (kProd)
+            prod *= py;
+        else
+            loss -= log_pos(py);
+        hits += hit ? 1 : 0;
         if (GRAD) {
-            // p_0 - y_0 = -(1 - p_y) if y = 0 else p_0: magnitude is the
-            // probability of the class that is not y, sign is - iff y = 0
-            const T mag = y_is_min ? inv : lo;
-            T d0 = y0 ? -mag : mag;
-            if (MASKED) d0 = valid ? d0 : T(0);
 #pragma unroll
-            for (int f = 0; f < F; ++f) acc[f] = fma(x[f], d0, acc[f]);
+            for (int f = 0; f < F; ++f) acc[f] = fma(x[f], q, acc[f]);
         }
+    }
+
+    // The first-maximum argmax of a tied row (t == 1): hit iff y == 0.
+    template <bool MASKED>
+    static __device__ __forceinline__ void fixup(const T (&x)[F], const T (&wd)[NB],
+                                                 const int32_t *ys, int r, bool valid, T &,
+                                                 int &hits) {
+        const T u = margin(x, wd);
+        const T t = exp_neg(fabs(u), MathConsts<T>());
+        if ((MASKED && !valid) || !(t == T(1))) return;
+        hits += (ys[r] == 0 ? 1 : 0) - (u > T(0) ? 1 : 0);
     }
 
     static __device__ __forceinline__ bool param_of(int m, int sub, int &j, T &sign) {
         j = 2 * m + sub;
-        sign = sub == 0 ? T(1) : T(-1);
+        sign = sub == 0 ? T(-1) : T(1);
         return sub < 2 && m < F;
     }
     static __device__ __forceinline__ int owner_lane(int j, int shift) {
@@ -487,30 +517,70 @@ struct TwoClassModel {
 };
 
 template <int F, int K>
-struct UseTwoClass { static constexpr bool value = (K == 2) && (F + 2 <= 32); };
+struct UseTwoClass { static constexpr bool value = signed_rows(F, K); };
 
-// UU chunks of 64 minibatch rows: minibatch row i -> dataset row order[i].
-template <typename Model, typename T, int F, bool MASKED, int UU, int NA>
+// Rows of one lane between log folds of `prod` (factors in (1e-16, 1]:
+// 16 of them stay above 1e-256).
+constexpr int kProdFold = 16;
+
+// UU chunks of 64 minibatch rows: minibatch row i -> dataset row order[i]
+// (ORDERED) or row i.  FIX runs Model::fixup on them instead of Model::row.
+template <typename Model, typename T, int F, bool MASKED, bool ORDERED, bool FIX, int UU, int NA>
 __device__ __forceinline__ void rows_block(const T *xs, const int32_t *ys, const int32_t *order,
-                                           int i, int B, const T (&w)[Model::NB],
-                                           const MathConsts<T> &mc, T (&acc)[NA]) {
+                                           int i, int B, const T (&w)[Model::NB], T (&acc)[NA],
+                                           T &loss, T &prod, int &hits,
+                                           typename Model::Watch &wt) {
     T x[UU][F];
-    int y[UU];
+    int r[UU];
     bool valid[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         const int iu = i + u * kWave;
         valid[u] = !MASKED || iu < B;
-        const int r = valid[u] ? (order ? order[iu] : iu) : 0;
-        load_row<T, F>(xs, r, x[u]);
-        y[u] = ys[r];
+        r[u] = valid[u] ? (ORDERED ? order[iu] : iu) : 0;
+        load_row<T, F>(xs, r[u], x[u]);
     }
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        T lt, hit;
-        Model::template row<true, MASKED>(x[u], w, y[u], valid[u], mc, acc, lt, hit);
-        acc[Model::NE] += lt;
-        acc[Model::NE + 1] += hit;
+        if constexpr (FIX)
+            Model::template fixup<MASKED>(x[u], w, ys, r[u], valid[u], loss, hits);
+        else
+            Model::template row<true, MASKED>(x[u], w, ys, r[u], valid[u], acc, loss, prod, hits,
+                                              wt);
+    }
+}
+
+// The minibatch pass: full groups of U chunks (64 rows each) run unmasked
+// with U independent dependency chains in flight; a ragged tail runs one
+// masked chunk at a time.  Then, only if some lane flagged a row, the
+// exact fix-up pass over the same rows.
+template <typename Model, typename T, int F, bool ORDERED, int NA>
+__device__ __forceinline__ void minibatch_pass(const T *xs, const int32_t *ys,
+                                               const int32_t *order, int lane, int B,
+                                               const T (&w)[Model::NB], T (&acc)[NA],
+                                               T &loss, int &hits) {
+    constexpr int U = sizeof(T) == 8 ? 1 : 4;
+    T prod = T(1);
+    int since = 0;
+    typename Model::Watch wt;
+    const int full = B / (kWave * U) * (kWave * U);
+    for (int i0 = 0; i0 < full; i0 += kWave * U) {
+        rows_block<Model, T, F, false, ORDERED, false, U>(xs, ys, order, i0 + lane, B, w, acc,
+                                                          loss, prod, hits, wt);
+        if (Model::kProd && (since += U) >= kProdFold) {
+            loss -= log_pos(prod);
+            prod = T(1);
+            since = 0;
+        }
+    }
+    for (int i0 = full; i0 < B; i0 += kWave)
+        rows_block<Model, T, F, true, ORDERED, false, 1>(xs, ys, order, i0 + lane, B, w, acc,
+                                                         loss, prod, hits, wt);
+    if (Model::kProd) loss -= log_pos(prod);
+    if (Model::kFixup && __any(wt.flagged())) {
+        for (int i0 = 0; i0 < B; i0 += kWave)
+            rows_block<Model, T, F, true, ORDERED, true, 1>(xs, ys, order, i0 + lane, B, w, acc,
+                                                            loss, prod, hits, wt);
     }
 }
 
@@ -572,17 +642,19 @@ __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
     const int N = a.N;
 
     // ---- per-env state loads first: their latency overlaps the staging copy.
-    T wl = T(0), al = T(0);
-    if (active && lane < P) {
-        wl = a.W[pbase + lane];
-        al = static_cast<T>(a.act[pbase + lane]);
-    }
+    // Unconditional loads from clamped indices (inactive lanes and waves
+    // read a valid element and discard it), so no branch separates a load
+    // from its use and nothing waits on them before the staging barrier.
     int j_own;
     T sign_own;
     const bool owner = Model::param_of(lane >> SHIFT, lane & ((1 << SHIFT) - 1), j_own, sign_own);
-    const T gprev = (active && owner) ? a.G[pbase + j_own] : T(0);
-    const double lprev = active ? a.L[e] : 0.0;
-    const int step_prev = active ? a.step[e] : 0;
+    const int eidx = active ? e : 0;
+    const int pl = lane < P ? lane : P - 1;
+    const T w_raw = a.W[pbase + pl];
+    const float a_raw = a.act[pbase + pl];
+    const T g_raw = a.G[pbase + (owner ? j_own : 0)];
+    const double lprev = a.L[eidx];
+    const int step_prev = a.step[eidx];
 
     // ---- dataset: [rows | labels] staged into LDS once per block (16-byte copies).
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -591,27 +663,22 @@ __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
     const T *xs;
     const int32_t *ys;
     if constexpr (STAGED) {
+        // LDS-DMA (global_load_lds_dwordx4): each wave-instruction copies one
+        // 1 KiB chunk straight into LDS (destination = chunk base + lane*16),
+        // with no VGPR round trip; all of a wave's chunks are in flight at
+        // once.  Every block reads the same few KB, so each block starts at
+        // a rotated chunk to spread the 32 CUs of an XCD over the L2 lines.
         const int nvec = static_cast<int>(align16_dev(xbytes + 4 * static_cast<size_t>(N)) / 16);
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.data);
-        uint4 *dst = reinterpret_cast<uint4 *>(smem);
-        // Every block reads the same few KB: rotate each block's starting
-        // vector so the 32 CUs of an XCD do not queue on the same L2 lines
-        // at the same moment; all of a thread's loads go out before the
-        // first LDS write.
-        constexpr int kBatch = 4;
-        const int rot = static_cast<int>((blockIdx.x * 97u) % static_cast<unsigned>(nvec));
-        for (int i0 = threadIdx.x; i0 < nvec; i0 += kBatch * kBlock) {
-            uint4 v[kBatch];
-            int idx[kBatch];
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b) {
-                const int i = i0 + b * kBlock;
-                idx[b] = i + rot < nvec ? i + rot : i + rot - nvec;
-                if (i < nvec) v[b] = src[idx[b]];
-            }
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b)
-                if (i0 + b * kBlock < nvec) dst[idx[b]] = v[b];
+        const int nch = (nvec + kWave - 1) / kWave;
+        const int rot = static_cast<int>((blockIdx.x * 5u) % static_cast<unsigned>(nch));
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        for (int c0 = wave; c0 < nch; c0 += kWavesPerBlock) {
+            const int c = c0 + rot < nch ? c0 + rot : c0 + rot - nch;   // wave-uniform
+            const int v = c * kWave + lane;
+            if (v < nvec)
+                __builtin_amdgcn_global_load_lds(
+                    (__attribute__((address_space(1))) void *)(a.data + static_cast<size_t>(v) * 16),
+                    (__attribute__((address_space(3))) void *)(smem + c * kWave * 16), 16, 0, 0);
         }
         __syncthreads();
         CE_STAMP(1);
@@ -624,7 +691,8 @@ __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
     if (!active) return;
 
     // ---- W <- W - a (optimize.py:74-75); lane j owns parameter j.
-    wl = wl - al;
+    const T gprev = owner ? g_raw : T(0);
+    T wl = lane < P ? w_raw - static_cast<T>(a_raw) : T(0);
     T w[Model::NB];
     Model::broadcast(wl, w);
     const int cur_step = __builtin_amdgcn_readfirstlane(step_prev) + 1;
@@ -639,14 +707,14 @@ __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
     T acc[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j) acc[j] = T(0);
-    // Full groups of U chunks (64 rows each) run unmasked with U independent
-    // dependency chains in flight; a ragged tail runs one masked chunk at a time.
-    constexpr int U = sizeof(T) == 8 ? 1 : 4;
-    const int full = a.B / (kWave * U) * (kWave * U);
-    for (int i0 = 0; i0 < full; i0 += kWave * U)
-        rows_block<Model, T, F, false, U>(xs, ys, order, i0 + lane, a.B, w, MathConsts<T>(), acc);
-    for (int i0 = full; i0 < a.B; i0 += kWave)
-        rows_block<Model, T, F, true, 1>(xs, ys, order, i0 + lane, a.B, w, MathConsts<T>(), acc);
+    T loss_l = T(0);
+    int hits_l = 0;
+    if (order)
+        minibatch_pass<Model, T, F, true>(xs, ys, order, lane, a.B, w, acc, loss_l, hits_l);
+    else
+        minibatch_pass<Model, T, F, false>(xs, ys, nullptr, lane, a.B, w, acc, loss_l, hits_l);
+    acc[NE] = loss_l;
+    acc[NE + 1] = static_cast<T>(hits_l);
     CE_STAMP(3);
     ReduceScatter<T, NP, 32>::run(acc, lane);
     const T tot_loss = readlane(acc[0], NE << SHIFT);
@@ -658,21 +726,36 @@ __global__ __launch_bounds__(kBlock) void optimize_step_kernel(StepArgs<T> a) {
     // the minibatch *is* the dataset and the reference computes the same
     // numbers twice, so they are reused.
     if (a.B != N) {
-        T fl = T(0), fh = T(0);
+        T fl = T(0), fprod = T(1);
+        int fh = 0, since = 0;
         T none[1];
+        typename Model::Watch wt;
         for (int i0 = 0; i0 < N; i0 += kWave) {
             const int r = i0 + lane;
             const bool valid = r < N;
             const int rr = valid ? r : 0;
             T x[F];
             load_row<T, F>(xs, rr, x);
-            T lt, hit;
-            Model::template row<false, true>(x, w, ys[rr], valid, MathConsts<T>(), none, lt, hit);
-            fl += lt;
-            fh += hit;
+            Model::template row<false, true>(x, w, ys, rr, valid, none, fl, fprod, fh, wt);
+            if (Model::kProd && ++since >= kProdFold) {
+                fl -= log_pos(fprod);
+                fprod = T(1);
+                since = 0;
+            }
+        }
+        if (Model::kProd) fl -= log_pos(fprod);
+        if (Model::kFixup && __any(wt.flagged())) {
+            for (int i0 = 0; i0 < N; i0 += kWave) {
+                const int r = i0 + lane;
+                const bool valid = r < N;
+                const int rr = valid ? r : 0;
+                T x[F];
+                load_row<T, F>(xs, rr, x);
+                Model::template fixup<true>(x, w, ys, rr, valid, fl, fh);
+            }
         }
         objective = static_cast<double>(wave_sum(fl)) / N;
-        accuracy = static_cast<double>(wave_sum(fh)) / N;
+        accuracy = static_cast<double>(wave_sum(static_cast<T>(fh))) / N;
     }
 
     CE_STAMP(4);

@@ -27,7 +27,7 @@ def main():
     p.add_argument('--precision', default='f64')
     p.add_argument('--steps', type=int, default=20)
     args = p.parse_args()
-    assert os.environ.get('CE_LIB') == 'diag', 'run with CE_LIB=diag'
+    assert os.environ.get('CE_LIB', '').startswith('diag'), 'run with CE_LIB=diag*'
     import torch
     from custom_envs_amd import _native
     from custom_envs_amd.data import load_data
