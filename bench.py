@@ -312,18 +312,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # live kernel duration: HIP events around individual launches on the
-    # engine's stream (= torch's current stream)
-    n_ev = 200
+    # live kernel duration: HIP events on the engine's stream (= torch's
+    # current stream) around graph replays of S back-to-back step launches,
+    # divided by S: the per-launch time on the stream, i.e. the kernel plus
+    # its share of the inter-kernel boundary (rocprofv3's kernel-only average
+    # is the same minus that gap; profiles/ holds both)
+    n_ev = 8
     eng.step_many_device(S, actions, out)   # backlog: events then time the kernels, not the host
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
     for i in range(n_ev):
         starts[i].record(stream)
-        eng.step_device(actions[i % S], out)
+        eng.step_many_device(S, actions, out)
         ends[i].record(stream)
     torch.cuda.synchronize()
-    times = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    times = [s.elapsed_time(e) / S for s, e in zip(starts, ends)]
     kernel_ms, kernel_ms_mean = float(np.median(times)), float(np.mean(times))
     phase_ms = {}
     if mlp and rank == 0:
@@ -449,8 +452,7 @@ def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, sh
             'traffic': _pmc_traffic(E, args.precision, 'optimize'),
             'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
             'kernel_ms_mean': kernel_ms_mean,
-            'kernel': 'ce::optimize_step_kernel<%s,10,2>' % (
-                'double' if args.precision == 'f64' else 'float'),
+            'kernel': 'ce::' + eng.step_kernel,
             # the limiter is the f64/f32 VALU, not HBM:
             # algorithmic FLOPs 2NFK (logits) + 2NFK (X^T(P-Y)) + 5NK
             'flops_per_env_step': flops,

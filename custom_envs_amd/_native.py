@@ -29,7 +29,7 @@ EXPORTS = (
     'ce_abi_version', 'ce_last_error', 'ce_create', 'ce_destroy', 'ce_set_stream',
     'ce_num_envs', 'ce_obs_dim', 'ce_act_dim', 'ce_seed', 'ce_seed_draws',
     'ce_seed_draws_mlp', 'ce_reset',
-    'ce_step', 'ce_step_async', 'ce_wait', 'ce_step_many', 'ce_host_outputs',
+    'ce_step', 'ce_step_async', 'ce_wait', 'ce_step_many', 'ce_host_outputs', 'ce_step_kernel',
     'ce_get_state', 'ce_set_state',
     'ce_multi_create', 'ce_multi_destroy', 'ce_multi_set_stream', 'ce_multi_reset',
     'ce_multi_step', 'ce_multi_step_async', 'ce_multi_wait', 'ce_multi_step_many',
@@ -100,6 +100,7 @@ def _declare(lib):
         'ce_wait': ([vp], ctypes.c_int),
         'ce_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeOutputs)], ctypes.c_int),
         'ce_host_outputs': ([vp, ctypes.POINTER(CeOutputs)], ctypes.c_int),
+        'ce_step_kernel': ([vp], ctypes.c_char_p),
         'ce_get_state': ([vp, ctypes.POINTER(CeState)], ctypes.c_int),
         'ce_set_state': ([vp, ctypes.POINTER(CeState)], ctypes.c_int),
         'ce_multi_create': ([ctypes.POINTER(CeMultiConfig), ctypes.POINTER(vp)], ctypes.c_int),

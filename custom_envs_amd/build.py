@@ -32,8 +32,8 @@ def sources():
 
 
 def headers():
-    return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'multiopt_kernels.h',
-                                            'mlp_kernels.h', 'common.h', 'seeding.h')] + [
+    return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'optimize_pair_kernel.h',
+                                            'multiopt_kernels.h', 'mlp_kernels.h', 'common.h', 'seeding.h')] + [
         os.path.join(ROOT, 'include', 'custom_envs_amd.h')]
 
 

@@ -23,6 +23,7 @@
 #include "common.h"
 #include "mlp_kernels.h"
 #include "optimize_kernels.h"
+#include "optimize_pair_kernel.h"
 #include "seeding.h"
 
 namespace {
@@ -38,6 +39,17 @@ void launch_step(const void *args, int grid, size_t lds, hipStream_t stream) {
                        *static_cast<const ce::StepArgs<T> *>(args));
 }
 
+// Two envs per wave (optimize_pair_kernel.h): grid = ceil(E / 16) blocks.
+template <typename T, int F, int K, int U>
+void launch_pair(const void *args, int, size_t lds, hipStream_t stream) {
+    if constexpr (ce::pair_shape(F, K)) {
+        const auto &a = *static_cast<const ce::StepArgs<T> *>(args);
+        const int grid = (a.E + ce::kPairEnvsPerBlock - 1) / ce::kPairEnvsPerBlock;
+        hipLaunchKernelGGL((ce::optimize_pair_kernel<T, F, U>), dim3(grid), dim3(ce::kPairBlock),
+                           lds + ce::pair_scratch_bytes<T>(F), stream, a);
+    }
+}
+
 template <typename T, int F, int K>
 void launch_reset(const void *args, int grid, size_t, hipStream_t stream) {
     hipLaunchKernelGGL((ce::optimize_reset_kernel<T, F, K>), dim3(grid), dim3(ce::kBlock), 0,
@@ -47,17 +59,21 @@ void launch_reset(const void *args, int grid, size_t, hipStream_t stream) {
 struct KernelEntry {
     int precision, F, K;
     StepFn step_staged, step_global, reset;
+    StepFn step_pair[2];   // U = 1, 2 (nullptr where the shape has no pair path)
 };
 
 // Shapes with a compiled register-path instance.
 #define CE_SHAPES(X) \
     X(2, 2) X(4, 2) X(4, 3) X(5, 2) X(8, 2) X(10, 2) X(16, 2) X(20, 2) X(10, 3) X(10, 4) X(3, 3)
 
+#define CE_PAIRS(T, F, K)                                                                   \
+    {ce::pair_shape(F, K) ? launch_pair<T, F, K, 1> : nullptr,                              \
+     ce::pair_shape(F, K) ? launch_pair<T, F, K, 2> : nullptr}
 #define CE_ENTRY(F, K)                                                                \
     {CE_F64, F, K, launch_step<double, F, K, true>, launch_step<double, F, K, false>, \
-     launch_reset<double, F, K>},                                                     \
+     launch_reset<double, F, K>, CE_PAIRS(double, F, K)},                             \
     {CE_F32, F, K, launch_step<float, F, K, true>, launch_step<float, F, K, false>,   \
-     launch_reset<float, F, K>},
+     launch_reset<float, F, K>, CE_PAIRS(float, F, K)},
 
 const KernelEntry kKernels[] = {CE_SHAPES(CE_ENTRY)};
 
@@ -97,6 +113,8 @@ struct ce_engine {
     float *h_act = nullptr;
     bool was_reset = false;
     bool staged = false;      // dataset fits the per-block LDS stage
+    StepFn pair = nullptr;    // two-envs-per-wave step kernel, when the shape has one
+    std::string kernel_name;  // what ce_step_kernel reports
     size_t stage_bytes = 0;
     // ce_step_many graph cache
     hipGraphExec_t graph = nullptr;
@@ -196,7 +214,8 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
         }
         return;
     }
-    StepFn fn = reset ? e->kern->reset : (e->staged ? e->kern->step_staged : e->kern->step_global);
+    StepFn fn = reset ? e->kern->reset
+                      : (e->pair ? e->pair : (e->staged ? e->kern->step_staged : e->kern->step_global));
     if (e->cfg.precision == CE_F64) {
         auto a = make_args<double>(e, act, o);
         fn(&a, grid_of(e), e->stage_bytes, stream);
@@ -464,6 +483,22 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     e->staged = e->stage_bytes <= ce::kStageLimit;
     if (const char *ns = std::getenv("CE_NO_STAGE"))   // experiment switch: rows from L1/L2
         if (ns[0] == '1') e->staged = false;
+    // Two envs per wave where the shape allows it.  U = rows each lane keeps
+    // in flight: 2 for float64 (its dependent-issue latency, ~10 cycles,
+    // needs the second chain at 2 waves per SIMD), 1 for float32; measured
+    // at 4096 envs.  CE_PAIR_U = 0 / 1 / 2 overrides (0 = one
+    // env per wave).
+    {
+        int u = cfg->precision == CE_F64 ? 2 : 1;
+        if (const char *pu = std::getenv("CE_PAIR_U")) u = std::atoi(pu);
+        if (e->staged && (u == 1 || u == 2)) e->pair = e->kern->step_pair[u - 1];
+        const std::string args = std::string(cfg->precision == CE_F64 ? "double" : "float") +
+                                 "," + std::to_string(cfg->n_features);
+        e->kernel_name = e->pair ? "optimize_pair_kernel<" + args + "," + std::to_string(u) + ">"
+                                 : "optimize_step_kernel<" + args + "," +
+                                       std::to_string(cfg->n_classes) +
+                                       (e->staged ? ",true>" : ",false>");
+    }
     }
     // Unseeded envs behave like np_random(None): os.urandom seeds.  The host
     // side normally seeds explicitly; default to seed = env index here.
@@ -606,6 +641,12 @@ int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
     }
     CE_HIP(hipGraphLaunch(e->graph, e->stream));
     return CE_OK;
+}
+
+const char *ce_step_kernel(const ce_engine *e) {
+    if (!e) return "";
+    if (e->mlp) return "mlp_train_kernel+mlp_info_kernel";
+    return e->kernel_name.c_str();
 }
 
 int ce_host_outputs(ce_engine *e, ce_outputs *view) {

@@ -81,6 +81,7 @@ class OptimizeEngine:
         self._lib = lib
         self._h = handle
         self.act_dim = lib.ce_act_dim(handle)
+        self.step_kernel = lib.ce_step_kernel(handle).decode()
         self.obs_dim = lib.ce_obs_dim(handle)
         view = CeOutputs()
         check(lib.ce_host_outputs(handle, ctypes.byref(view)), 'ce_host_outputs')

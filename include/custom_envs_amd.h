@@ -165,6 +165,11 @@ int ce_step_many(ce_engine *eng, int32_t k, const float *actions,
 /* Pinned host buffers holding the last host-mode outputs (zero-copy views). */
 int ce_host_outputs(ce_engine *eng, ce_outputs *view);
 
+/* Name of the step kernel the engine launches (introspection for profiles:
+ * "optimize_pair_kernel<double,10,2>", "optimize_step_kernel<...>", ...).
+ * Static storage, valid for the engine's lifetime; "" for a null engine. */
+const char *ce_step_kernel(const ce_engine *eng);
+
 int ce_get_state(ce_engine *eng, const ce_state *st);
 int ce_set_state(ce_engine *eng, const ce_state *st);
 

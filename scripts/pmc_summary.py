@@ -20,7 +20,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = 'optimize_step_kernel'
+KERNELS = ('optimize_pair_kernel', 'optimize_step_kernel')   # the engine's step kernels
 
 
 def main():
@@ -29,15 +29,16 @@ def main():
     p.add_argument('--envs', type=int, default=4096)
     p.add_argument('--precision', default='f64')
     p.add_argument('--bytes-per-env-step', type=int, default=925)
+    p.add_argument('--tag', default='', help='suffix of the summary file name')
     args = p.parse_args()
     out_dir = os.path.join(ROOT, 'profiles')
     os.makedirs(out_dir, exist_ok=True)
     stats = os.path.join(ROOT, 'gpurun_out', 'prof', 'run_kernel_stats.csv')
     summary = {'round': args.round, 'envs': args.envs, 'precision': args.precision}
     if os.path.exists(stats):
-        shutil.copy(stats, os.path.join(out_dir, '%s_kernel_stats.csv' % args.round))
+        shutil.copy(stats, os.path.join(out_dir, '%s_kernel_stats%s.csv' % (args.round, args.tag)))
         for row in csv.DictReader(open(stats)):
-            if KERNEL in row['Name']:
+            if any(k in row['Name'] for k in KERNELS):
                 summary['kernel'] = row['Name']
                 summary['kernel_avg_ns'] = float(row['AverageNs'])
                 summary['kernel_calls'] = int(row['Calls'])
@@ -45,7 +46,7 @@ def main():
     for path in sorted(glob.glob(os.path.join(ROOT, 'gpurun_out', 'pmc', 'p*',
                                               'run_counter_collection.csv'))):
         for row in csv.DictReader(open(path)):
-            if KERNEL in row['Kernel_Name']:
+            if any(k in row['Kernel_Name'] for k in KERNELS):
                 counters[row['Counter_Name']].append(float(row['Counter_Value']))
     means = {k: sum(v) / len(v) for k, v in counters.items()}
     summary['pmc_mean_per_dispatch'] = means
@@ -65,7 +66,7 @@ def main():
                     'SQ_ACTIVE_INST_VALU'):
             if key in means:   # quad-cycles per the microarch guide
                 summary[key.lower() + '_cycles_per_wave'] = 4 * means[key] / waves
-    with open(os.path.join(out_dir, '%s_pmc.json' % args.round), 'w') as fh:
+    with open(os.path.join(out_dir, '%s_pmc%s.json' % (args.round, args.tag)), 'w') as fh:
         json.dump(summary, fh, indent=1, sort_keys=True)
     with open(os.path.join(out_dir, 'pmc_latest.json'), 'w') as fh:
         json.dump(summary, fh, indent=1, sort_keys=True)
