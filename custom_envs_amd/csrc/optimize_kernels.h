@@ -25,10 +25,12 @@
 //   - Minibatch row i of an env lives on lane i % 64 (chunks of 64 rows).
 //   - W is broadcast from lanes 0..P-1 into scalar registers (v_readlane):
 //     the row loop is VGPR(x) x SGPR(w) FMAs.
-//   - K = 2 (the benchmark problem) uses the two-class form of the same
-//     softmax: z = x.(w0 - w1), t = exp(-|z|), p_max = 1/(1+t),
-//     p_min = t/(1+t): one exp, one reciprocal and one log per row, and
-//     column 1 of X^T(P-Y) is exactly minus column 0.
+//   - K = 2 uses the two-class form of the same softmax (TwoClassModel):
+//     z = x.(w0 - w1), t = exp(-|z|), p_max = 1/(1+t), p_min = t/(1+t): one
+//     exp and one reciprocal per row, the cross-entropy as the log of a
+//     per-lane product, and column 1 of X^T(P-Y) is exactly minus column 0.
+//     The benchmark shape runs the two-envs-per-wave variant of this kernel
+//     (optimize_pair_kernel.h); this one-env-per-wave kernel covers the rest.
 //   - p_y - 1 is formed as -(sum of the other classes' p), which is the
 //     same number without the cancellation.
 //   - Gradient partials, the loss and the hit count are combined by a
