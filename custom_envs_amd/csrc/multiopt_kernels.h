@@ -33,6 +33,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "optimize_kernels.h"   // xchg<>: DPP / swizzle lane exchanges
+
 namespace ce {
 
 constexpr int kRawHist = 5;
@@ -67,11 +69,42 @@ struct Group {
     static constexpr int G = P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : 16;
 };
 
-template <int G, typename T>
+// Sum over a group of G lanes by an xor butterfly on DPP / ds_swizzle
+// exchanges (no LDS round trip): every lane of the group gets the total.
+template <int G, typename T, int OFF = G / 2>
 __device__ __forceinline__ T group_sum(T v) {
-#pragma unroll
-    for (int off = G / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off, G);
-    return v;
+    if constexpr (OFF == 0) {
+        return v;
+    } else {
+        v = v + xchg<OFF>(v);
+        return group_sum<G, T, OFF / 2>(v);
+    }
+}
+
+// Lane SRC of each G-lane group, broadcast to the group (G <= 4: DPP
+// quad_perm; wider groups: ds_bpermute).
+template <int G, int SRC>
+__device__ __forceinline__ float group_bcast(float v) {
+    if constexpr (G == 4) {
+        return __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), SRC * 0x55,
+                                                           0xf, 0xf, false));
+    } else if constexpr (G == 2) {
+        constexpr int c = SRC | (SRC << 2) | ((2 + SRC) << 4) | ((2 + SRC) << 6);
+        return __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), c, 0xf, 0xf,
+                                                           false));
+    } else {
+        return __shfl(v, SRC, G);
+    }
+}
+
+template <int G, int P, int Q = 0>
+__device__ __forceinline__ float pair_terms_sum(float loss, float term) {
+    // loss + term(pair 0) + term(pair 1) + ..., left to right (TF1's add order)
+    if constexpr (Q >= P / 2) {
+        return loss;
+    } else {
+        return pair_terms_sum<G, P, Q + 1>(loss + group_bcast<G, 2 * Q>(term), term);
+    }
 }
 
 // Sum of Rosenbrock over coordinate pairs in float32, with TF1's autodiff
@@ -83,7 +116,7 @@ template <int P>
 __device__ __forceinline__ void rosenbrock_lane(float th, int i, float &g, float &loss) {
 #pragma clang fp contract(off)
     constexpr int G = Group<P>::G;
-    const float other = __shfl_xor(th, 1, G);
+    const float other = xchg<1>(th);
     const bool is_x = (i & 1) == 0;
     const float x = is_x ? th : other, y = is_x ? other : th;
     const float d = y - x * x;
@@ -91,9 +124,7 @@ __device__ __forceinline__ void rosenbrock_lane(float th, int i, float &g, float
     const float term = 100.0f * (d * d) + r * r;
     const float t = 200.0f * d;
     g = is_x ? -((2.0f * t) * x) - 2.0f * r : t;
-    loss = 0.0f;
-#pragma unroll
-    for (int p = 0; p < P / 2; ++p) loss = loss + __shfl(term, 2 * p, G);
+    loss = pair_terms_sum<G, P>(0.0f, term);
 }
 
 // numpy.nan_to_num of a / |b| in float64.
@@ -167,33 +198,61 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     const int ic = i < P ? i : 0;
     const int r = a.agent_row[ic];
 
-    const int s = a.step[ec] + 1;
-    // ---- update (multioptlrs.py:81-87), lr = 10^(a - 4): the exponent rounds
-    // to float32 first; the power is taken in float64 and rounded once
-    const float x = a.act[ec * P + r] - 4.0f;
-    const float lr = static_cast<float>(pow(10.0, static_cast<double>(x)));
+    // ---- every load of the step up front: no address depends on another
+    // load (the ring slots are picked from registers once `step` is in), so
+    // the wave waits for memory once instead of once per dependent round trip
+    const int step_prev = a.step[ec];
+    const float act = a.act[ec * P + r];
     const float th0 = a.theta[ec * P + ic];
     const float g0 = a.grad[ec * P + ic];
+    float hl_v[kRawHist], hg_v[kRawHist], hw_v[kRawHist];
+#pragma unroll
+    for (int k = 0; k < kRawHist; ++k) {
+        hl_v[k] = a.hl[k * E + ec];
+        hg_v[k] = a.hg[(k * E + ec) * P + ic];
+        hw_v[k] = a.hw[(k * E + ec) * P + ic];
+    }
+    double al_v[kMultiStageH], ag_v[kMultiStageH], aw_v[kMultiStageH];
+#pragma unroll
+    for (int j = 0; j < kMultiStageH; ++j) {
+        if (j < H) {                             // wave-uniform
+            al_v[j] = a.al[j * E + ec];
+            ag_v[j] = a.ag[(j * E + ec) * P + ic];
+            aw_v[j] = a.aw[(j * E + ec) * P + ic];
+        }
+    }
+
+    const int s = step_prev + 1;
+    // ---- update (multioptlrs.py:81-87), lr = 10^(a - 4): the exponent rounds
+    // to float32 first; the power is taken in float64 and rounded once
+    const float x = act - 4.0f;
+    const float lr = static_cast<float>(exp10(static_cast<double>(x)));
     const float th = th0 - g0 * lr;
     float g, loss;
     rosenbrock_lane<P>(th, i, g, loss);
 
     // ---- raw history append, observation v3 against the previous entry
     const int slot = s % kRawHist, prev = (s - 1) % kRawHist;
-    const double l_prev = a.hl[prev * E + ec];
-    const float gp = a.hg[(prev * E + ec) * P + ic];
-    const float wp = a.hw[(prev * E + ec) * P + ic];
+    double l_prev = 0.0;
+    float gp = 0.0f, wp = 0.0f;
+    // info sums over the raw ring: this step's entry, then the other four in
+    // slot order (the entries being replaced are the loaded ones)
+    double lsum = loss, gsum = g;
+#pragma unroll
+    for (int k = 0; k < kRawHist; ++k) {
+        if (k == prev) {
+            l_prev = hl_v[k];
+            gp = hg_v[k];
+            wp = hw_v[k];
+        }
+        if (k != slot) {
+            lsum += hl_v[k];
+            gsum += hg_v[k];
+        }
+    }
     const double adj_l = ratio(loss, l_prev);
     const double adj_g = ratio(g, gp);
     const double adj_w = ratio(th, wp);
-    // info sums over the raw ring: this step's entry from registers, the
-    // other four from memory (read before this step's slot is overwritten)
-    double lsum = loss, gsum = g;
-    for (int k = 0; k < kRawHist; ++k) {
-        if (k == slot) continue;
-        lsum += a.hl[k * E + ec];
-        gsum += a.hg[(k * E + ec) * P + ic];
-    }
     const int aslot = (s - 1) % H;
     if (on) {
         a.hg[(slot * E + e) * P + i] = g;
@@ -221,15 +280,17 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     const int span = 64 / G * P * row;       // floats of one wave's env block
     float *lds = stage + wave * span;
     float *dst = staged ? lds + ((lane / G) * P + r) * row : a.obs + (ec * P + r) * row;
+    // slot j holds the entry of age k = (s - 1 - j) mod H (age 0 = this
+    // step's, written above); ages >= s are the reset zeros
     double st_abs = 0.0;
-    for (int k = 0; k < H; ++k) {
-        double wk = adj_w, gk = adj_g, lk = adj_l;  // k = 0: this step's entry
-        if (k > 0) {
-            const bool live = k < s;                // older slots are reset zeros
-            const int sl = ((s - 1 - k) % H + H) % H;
-            wk = live ? a.aw[(sl * E + ec) * P + ic] : 0.0;
-            gk = live ? a.ag[(sl * E + ec) * P + ic] : 0.0;
-            lk = live ? a.al[sl * E + ec] : 0.0;
+    auto put = [&](int j, double wk, double gk, double lk) {
+        const int k = ((s - 1 - j) % H + H) % H;
+        if (k == 0) {
+            wk = adj_w;
+            gk = adj_g;
+            lk = adj_l;
+        } else if (k >= s) {
+            wk = gk = lk = 0.0;
         }
         st_abs += fabs(wk) + fabs(gk) + fabs(lk);
         if (on) {
@@ -237,7 +298,12 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
             dst[H + k] = wipe ? -1.0f : static_cast<float>(clip100(lk) - 1.0);
             dst[2 * H + k] = wipe ? -1.0f : static_cast<float>(clip100(gk) - 1.0);
         }
-    }
+    };
+#pragma unroll
+    for (int j = 0; j < kMultiStageH; ++j)
+        if (j < H) put(j, aw_v[j], ag_v[j], al_v[j]);
+    for (int j = kMultiStageH; j < H; ++j)       // long histories: loaded here
+        put(j, a.aw[(j * E + ec) * P + ic], a.ag[(j * E + ec) * P + ic], a.al[j * E + ec]);
     if (staged) {
         // the wave's rows are obs[e_first * P * row ...] contiguous
         __syncthreads();                        // every thread gets here (no early exit)
