@@ -196,7 +196,10 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     const int row = 3 * H;
     const size_t ec = env_ok ? e : 0;          // clamp so idle lanes read valid memory
     const int ic = i < P ? i : 0;
-    const int r = a.agent_row[ic];
+    // sorted agent names ('parameter-0', 'parameter-1', 'parameter-10', ...)
+    // only reorder rows from P = 11 on; below that the row is the agent
+    // index and the action load does not wait for the kernarg table
+    const int r = P <= 10 ? ic : a.agent_row[ic];
 
     // ---- every load of the step up front: no address depends on another
     // load (the ring slots are picked from registers once `step` is in), so
