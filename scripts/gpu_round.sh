@@ -24,3 +24,12 @@ for CTRS in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VAL
   timeout -s KILL 120 rocprofv3 --pmc $CTRS -d $OUT/pmc/p$i -o run --output-format csv -- python3 bench.py --profile-only --steps 500 --warmup 50 ${BENCH_ARGS:-} > $OUT/pmc/p$i.log 2>&1; rc=$?
   echo "pmc pass $i rc=$rc"; fatal $rc
 done
+# config 5 and config 3 lines + their kernel traces (secondary workloads)
+timeout -k 10 300 python bench.py --workload multi > $OUT/bench_multi.log 2>&1; rc=$?
+echo "bench multi rc=$rc"; tail -1 $OUT/bench_multi.log | cut -c1-200; fatal $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_multi -o run --output-format csv -- python3 bench.py --workload multi --profile-only --steps 2000 --warmup 100 > $OUT/prof_multi.log 2>&1; rc=$?
+echo "rocprof multi rc=$rc"; fatal $rc
+timeout -k 10 400 python bench.py --workload mlp --steps 20 --warmup 4 --cpu-seconds 10 > $OUT/bench_mlp.log 2>&1; rc=$?
+echo "bench mlp rc=$rc"; tail -1 $OUT/bench_mlp.log | cut -c1-200; fatal $rc
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_mlp -o run --output-format csv -- python3 bench.py --workload mlp --profile-only --steps 10 --warmup 2 > $OUT/prof_mlp.log 2>&1; rc=$?
+echo "rocprof mlp rc=$rc"; fatal $rc
