@@ -47,6 +47,36 @@ def test_history_matches_reference(impl):
         assert a.build_multistate() == b.build_multistate()
 
 
+def test_rosenbrock_terms_match_reference_function():
+    """The oracle's float32 Rosenbrock pair terms are bit-identical to the
+    reference's own ``compute_rosenbrock`` (utils_functions.py:4-6, imported
+    by path) on float32 inputs: numpy evaluates 100*(y - x**2)**2 + (1 - x)**2
+    in the same float32 operation order (x**2 is x*x)."""
+    path = os.path.join(REFERENCE, 'custom_envs', 'utils', 'utils_functions.py')
+    if not os.path.exists(path):
+        pytest.skip('reference checkout not present')
+    spec = importlib.util.spec_from_file_location('ref_utils_functions', path)
+    ref = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ref)
+    from oracle.multioptlrs import RosenbrockPairs
+    rs = np.random.RandomState(11)
+    prob = RosenbrockPairs(ndims=8)
+    for scale in (0.5, 2.0, 30.0):
+        p = (rs.normal(size=8) * scale).astype(np.float32)
+        x, y = p[0::2], p[1::2]
+        ref_terms = ref.compute_rosenbrock(x, y)
+        assert ref_terms.dtype == np.float32
+        one, c100 = np.float32(1), np.float32(100)
+        d = y - x * x
+        ours = c100 * (d * d) + (one - x) * (one - x)
+        assert np.array_equal(ours, ref_terms)
+        loss = np.float32(0)
+        for term in ref_terms:
+            loss = np.float32(loss + term)
+        prob.params = p.copy()
+        assert prob._eval(p)[1] == loss
+
+
 @pytest.mark.parametrize('name,ndims,max_batches,hist,steps,seed,low,high', [
     ('multi_func2_h5', 2, 400, 5, 150, 7, -1.0, 0.5),
     ('multi_func4_h5', 4, 400, 5, 60, 8, 1.0, 3.0),
