@@ -43,15 +43,16 @@ def _dataset(n_features, n_rows=200, seed=3):
 
 def _rollout(dataset, pair_u, num_envs, batch_size, steps=43):
     from custom_envs_amd.engine import OptimizeEngine
-    old = os.environ.get('CE_PAIR_U')
+    saved = {k: os.environ.get(k) for k in ('CE_PAIR_U',)}
     os.environ['CE_PAIR_U'] = str(pair_u)
     try:
         eng = OptimizeEngine(*dataset, num_envs=num_envs, batch_size=batch_size)
     finally:
-        if old is None:
-            os.environ.pop('CE_PAIR_U')
-        else:
-            os.environ['CE_PAIR_U'] = old
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
     P = eng.act_dim
     seeds = [77 + 5 * i for i in range(num_envs)]
     acts = np.random.RandomState(num_envs).normal(0, 0.05, (steps, num_envs, P)).astype(np.float32)
@@ -81,8 +82,9 @@ def _check_against_oracle(dataset, batch_size, seeds, acts, outs, envs):
 
 
 @pytest.mark.parametrize('pair_u', [0, 1, 2])
-@pytest.mark.parametrize('batch_size', [None, 32])
+@pytest.mark.parametrize('batch_size', [None, 32, 100])
 def test_paths_match_oracle_f10(pair_u, batch_size):
+    """batch_size 100: a masked tail of minibatch rows (100 = 3 x 32 + 4)."""
     ds = _dataset(10)
     E = 37
     seeds, acts, outs = _rollout(ds, pair_u, E, batch_size)
