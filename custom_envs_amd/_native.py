@@ -34,6 +34,9 @@ EXPORTS = (
     'ce_multi_create', 'ce_multi_destroy', 'ce_multi_set_stream', 'ce_multi_reset',
     'ce_multi_step', 'ce_multi_step_async', 'ce_multi_wait', 'ce_multi_step_many',
     'ce_multi_host_outputs', 'ce_multi_get_state',
+    'ce_nn_create', 'ce_nn_destroy', 'ce_nn_set_stream', 'ce_nn_n_params', 'ce_nn_seed',
+    'ce_nn_seed_draws', 'ce_nn_reset', 'ce_nn_step', 'ce_nn_step_async', 'ce_nn_wait',
+    'ce_nn_step_many', 'ce_nn_host_outputs', 'ce_nn_get_state',
 )
 
 CE_FUNC_ROSENBROCK_PAIRS = 0
@@ -69,6 +72,16 @@ class CeMultiOutputs(ctypes.Structure):
     _fields_ = [('obs', ctypes.c_void_p), ('reward', ctypes.c_void_p),
                 ('done', ctypes.c_void_p), ('info', ctypes.c_void_p),
                 ('episode_len', ctypes.c_void_p)]
+
+
+CE_NN_MAX_HIDDEN = 4
+
+
+class CeNnConfig(ctypes.Structure):
+    _fields_ = ([(name, ctypes.c_int32) for name in (
+        'abi_version', 'device', 'num_envs', 'n_rows', 'n_features', 'n_classes',
+        'batch_size', 'n_hidden')] + [('hidden', ctypes.c_int32 * CE_NN_MAX_HIDDEN)] +
+        [(name, ctypes.c_int32) for name in ('max_history', 'max_batches', 'auto_reset')])
 
 
 class CeState(ctypes.Structure):
@@ -113,6 +126,19 @@ def _declare(lib):
         'ce_multi_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
         'ce_multi_host_outputs': ([vp, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
         'ce_multi_get_state': ([vp, vp, vp], ctypes.c_int),
+        'ce_nn_create': ([ctypes.POINTER(CeNnConfig), vp, vp, ctypes.POINTER(vp)], ctypes.c_int),
+        'ce_nn_destroy': ([vp], None),
+        'ce_nn_set_stream': ([vp, vp], ctypes.c_int),
+        'ce_nn_n_params': ([vp], ctypes.c_int),
+        'ce_nn_seed': ([vp, vp, i32], ctypes.c_int),
+        'ce_nn_seed_draws': ([ctypes.c_uint64, i32, vp, i32, vp, vp, vp], ctypes.c_int),
+        'ce_nn_reset': ([vp, ctypes.POINTER(CeMultiOutputs), u32], ctypes.c_int),
+        'ce_nn_step': ([vp, vp, ctypes.POINTER(CeMultiOutputs), u32], ctypes.c_int),
+        'ce_nn_step_async': ([vp, vp, ctypes.POINTER(CeMultiOutputs), u32], ctypes.c_int),
+        'ce_nn_wait': ([vp], ctypes.c_int),
+        'ce_nn_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
+        'ce_nn_host_outputs': ([vp, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
+        'ce_nn_get_state': ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

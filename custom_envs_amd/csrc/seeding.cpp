@@ -258,3 +258,36 @@ void reset_draws_mlp(uint64_t seed, int n_features, int n_hidden, int n_classes,
 }
 
 }  // namespace ce
+
+namespace ce {
+
+void reset_draws_nn(uint64_t seed, int n_dims, const int *dims, int n_rows, float *init_weights,
+                    int32_t *reset_perm, int32_t *epoch_perm) {
+    uint32_t key[2];
+    const int key_len = seed_key(seed, key);
+    Mt19937 rng;
+    rng.init_by_array(key, key_len);
+    size_t off = 0;
+    for (int l = 0; l + 1 < n_dims; ++l) {
+        const int fan_in = dims[l], fan_out = dims[l + 1];
+        const double limit = std::sqrt(6.0 / static_cast<double>(fan_in + fan_out));
+        const double low = -limit, range = limit - low;
+        const size_t n = static_cast<size_t>(fan_in) * fan_out;
+        for (size_t i = 0; i < n; ++i) {
+            const double v = low + range * rng.next_double();
+            if (init_weights) init_weights[off + i] = static_cast<float>(v);
+        }
+        off += n;
+        if (init_weights)
+            for (int i = 0; i < fan_out; ++i) init_weights[off + i] = 0.0f;
+        off += fan_out;
+    }
+    if (reset_perm) legacy_shuffle(rng, n_rows, reset_perm);
+    if (epoch_perm) {
+        Mt19937 fresh;
+        fresh.init_by_array(key, key_len);
+        legacy_shuffle(fresh, n_rows, epoch_perm);
+    }
+}
+
+}  // namespace ce

@@ -36,4 +36,13 @@ void reset_draws(uint64_t seed, int n_features, int n_classes, int n_rows,
 void reset_draws_mlp(uint64_t seed, int n_features, int n_hidden, int n_classes, int n_rows,
                      float *init_weights, int32_t *perm);
 
+// MultiOptLRs over the OptimizeNN problem (oracle/multinn.py nn_draws):
+// glorot-uniform kernels of every layer (dims[0] -> dims[1] -> ...) as legacy
+// uniform(-l, l) draws rounded to float32, zero biases, flat order
+// [W1 | b1 | W2 | b2 | ...]; then the reset's legacy shuffle of arange(N);
+// epoch_perm is the first shuffle of a fresh copy of the seed's stream (the
+// one every epoch end inside a step draws).  Any output may be null.
+void reset_draws_nn(uint64_t seed, int n_dims, const int *dims, int n_rows, float *init_weights,
+                    int32_t *reset_perm, int32_t *epoch_perm);
+
 }  // namespace ce

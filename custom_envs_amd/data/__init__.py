@@ -11,6 +11,11 @@ IDX archives) is a git-LFS pointer, so only the synthetic sets are served:
   mnist_synthetic    "MNIST-sized" features for the MLP config:
                      RandomState(0).rand(1024, 784), labels argmax(X T) with
                      T = RandomState(1).normal(size=(784, 10))
+  iris_synthetic     iris-shaped stand-in for 'iris' (load_data's default,
+                     the data set of get_problem('nn')): 150 rows, 4
+                     features, 3 classes of 50, Gaussian blobs at the iris
+                     class means/spreads from RandomState(0), then the iris
+                     branch's normalize + to_onehot (load_data.py:61-64)
 """
 import numpy as np
 
@@ -40,10 +45,30 @@ def _mnist_synthetic(num_of_labels=None):
     return features, to_onehot(labels, num_of_labels or 10)[0]
 
 
+def normalize(data):
+    """utils_math.py:77-87: per column (x - min) / (max - min + 1e-8)."""
+    mins, maxes = np.min(data, axis=0), np.max(data, axis=0)
+    return (data - mins) / (maxes - mins + 1e-8)
+
+
+_IRIS_MEANS = ((5.006, 3.428, 1.462, 0.246), (5.936, 2.770, 4.260, 1.326),
+               (6.588, 2.974, 5.552, 2.026))
+_IRIS_STDS = ((0.352, 0.379, 0.174, 0.105), (0.516, 0.314, 0.470, 0.198),
+              (0.636, 0.322, 0.552, 0.275))
+
+
+def _iris_synthetic(num_of_labels=None):
+    rs = np.random.RandomState(0)
+    features = np.concatenate([rs.normal(m, s, (50, 4)) for m, s in zip(_IRIS_MEANS, _IRIS_STDS)])
+    labels = np.repeat(np.arange(3), 50)
+    return normalize(features), to_onehot(labels, num_of_labels)[0]
+
+
 LOADERS = {
     'random_gaussians': lambda n: _gaussians(),
     'gaussians_256x10': lambda n: _gaussians(n_samples=256, n_features=10, random_state=0),
     'mnist_synthetic': _mnist_synthetic,
+    'iris_synthetic': _iris_synthetic,
 }
 
 

@@ -5,14 +5,20 @@ A single env is a one-env view of the HIP engine with auto-reset off; the
 vector path is ``custom_envs_amd.vectorize.OptVecEnv``.  Same constructor
 keywords (``problem``, ``max_batches``, ``max_history``), same Dict spaces
 keyed 'parameter-i', same 14 info keys.  ``problem`` is 'func' (the
-reference default: 2-D Rosenbrock from [-1.9, 2.0]) or 'func4' (the configs'
-4-D sum of two Rosenbrocks); ``initial_points`` overrides the start.
+reference default: 2-D Rosenbrock from [-1.9, 2.0]), 'func4' (the configs'
+4-D sum of two Rosenbrocks; ``initial_points`` overrides the start) or 'nn'
+(get_problem('nn'): the OptimizeNN network, one agent per parameter;
+``data_set`` is an InMemoryDataSet -- default the iris-shaped stand-in of
+load_data() -- and ``hidden`` the create_neural_net layers, default
+(256, 256)).
 """
+import os
+
 import numpy as np
 
 from custom_envs_amd import _native
 from custom_envs_amd.core import Env
-from custom_envs_amd.multi_engine import MultiOptEngine, agent_names, resolve_problem
+from custom_envs_amd.multi_engine import agent_names, create_engine
 from custom_envs_amd.spaces import Box, Dict
 
 
@@ -35,12 +41,13 @@ class MultiOptLRs(Env):
     AGENT_FMT = 'parameter-{:d}'
 
     def __init__(self, problem='func', max_batches=400, max_history=5, initial_points=None,
-                 device=0):
+                 device=0, data_set=None, hidden=None):
         self.spec_kwargs = {'problem': problem, 'max_batches': max_batches,
                             'max_history': max_history, 'initial_points': initial_points}
-        ndims, _ = resolve_problem(problem, initial_points)
-        self.engine = MultiOptEngine(1, problem, max_batches, max_history, initial_points,
-                                     device=device, auto_reset=False)
+        if problem == 'nn':
+            self.spec_kwargs.update(data_set=data_set, hidden=hidden)
+        self.engine = create_engine(1, device=device, auto_reset=False, **self.spec_kwargs)
+        ndims = self.engine.n_params
         self.max_batches, self.max_history = max_batches, max_history
         self.names = agent_names(ndims)
         self.observation_space, self.action_space = multi_spaces(ndims, max_history)
@@ -52,6 +59,15 @@ class MultiOptLRs(Env):
 
     def _states(self, obs):
         return {self.names[agent]: obs[r].copy() for r, agent in enumerate(self._rows)}
+
+    def seed(self, seed=None):
+        """BaseEnvironment.seed (baseenvironment.py:20-28): None draws a seed
+        from os.urandom, as gym's np_random does.  Only the 'nn' problem
+        draws anything (its initial weights and shuffles)."""
+        if seed is None:
+            seed = int.from_bytes(os.urandom(8), 'little')
+        self.engine.seed([seed])
+        return [seed]
 
     def reset(self):
         self.current_step = 0

@@ -35,8 +35,7 @@ def row_agents(n_params):
 def resolve_problem(problem, initial_points=None):
     if isinstance(problem, str):
         if problem not in PROBLEMS:
-            raise RuntimeError('Not a name of a problem: %r (the TF "nn" problem is out of '
-                               'scope for the GPU engine)' % problem)
+            raise RuntimeError('Not a name of a problem: %r' % problem)
         ndims, start = PROBLEMS[problem]
     else:
         ndims = int(problem.get('ndims', 2))
@@ -71,11 +70,20 @@ class MultiOptEngine:
             cfg.initial_points[i] = v
         handle = ctypes.c_void_p()
         check(lib.ce_multi_create(ctypes.byref(cfg), ctypes.byref(handle)), 'ce_multi_create')
-        self._lib, self._h = lib, handle
-        self.row_agents = row_agents(ndims)
+        self._lib, self._h, self._prefix = lib, handle, 'ce_multi_'
+        self._bind_outputs()
+
+    def _fn(self, name):
+        return getattr(self._lib, self._prefix + name)
+
+    def _call(self, name, *args):
+        return check(self._fn(name)(self._h, *args), self._prefix + name)
+
+    def _bind_outputs(self):
+        self.row_agents = row_agents(self.n_params)
         view = CeMultiOutputs()
-        check(lib.ce_multi_host_outputs(handle, ctypes.byref(view)), 'ce_multi_host_outputs')
-        E, P, W = self.num_envs, ndims, 3 * self.max_history
+        self._call('host_outputs', ctypes.byref(view))
+        E, P, W = self.num_envs, self.n_params, 3 * self.max_history
         n_info = len(_native.MULTI_INFO_KEYS)
         self._host = {
             'obs': _view(view.obs, E * P * W, ctypes.c_float, np.float32, (E * P, W)),
@@ -96,17 +104,16 @@ class MultiOptEngine:
         return self.num_envs * self.n_params
 
     def reset(self):
-        check(self._lib.ce_multi_reset(self._h, None, 0), 'ce_multi_reset')
+        self._call('reset', None, 0)
         return self._host['obs'].copy()
 
     def step_async(self, actions):
         actions = np.ascontiguousarray(actions, dtype=np.float32).reshape(self.rows)
         self._pending = actions
-        check(self._lib.ce_multi_step_async(self._h, actions.ctypes.data, None, 0),
-              'ce_multi_step_async')
+        self._call('step_async', actions.ctypes.data, None, 0)
 
     def step_wait(self):
-        check(self._lib.ce_multi_wait(self._h), 'ce_multi_wait')
+        self._call('wait')
         self._pending = None
         return self._host
 
@@ -116,8 +123,7 @@ class MultiOptEngine:
 
     # ------------------------------------------------------------- device mode
     def set_stream(self, stream_handle):
-        check(self._lib.ce_multi_set_stream(self._h, ctypes.c_void_p(stream_handle or 0)),
-              'ce_multi_set_stream')
+        self._call('set_stream', ctypes.c_void_p(stream_handle or 0))
 
     def output_fields(self):
         """(name, torch dtype, rows per env, trailing shape) of the step outputs."""
@@ -143,26 +149,23 @@ class MultiOptEngine:
 
     def reset_device(self, out):
         o = self._outputs(out)
-        check(self._lib.ce_multi_reset(self._h, ctypes.byref(o), _native.CE_PTR_DEVICE),
-              'ce_multi_reset')
+        self._call('reset', ctypes.byref(o), _native.CE_PTR_DEVICE)
 
     def step_device(self, actions, out):
         if actions.numel() < self.rows or not actions.is_contiguous():
             raise ValueError('actions must be a contiguous float32 tensor of E*P rows')
         o = self._outputs(out)
-        check(self._lib.ce_multi_step_async(self._h, actions.data_ptr(), ctypes.byref(o),
-                                            _native.CE_PTR_DEVICE), 'ce_multi_step_async')
+        self._call('step_async', actions.data_ptr(), ctypes.byref(o), _native.CE_PTR_DEVICE)
 
     def step_many_device(self, k, actions, out, per_step_actions=True):
         if actions.numel() < (k if per_step_actions else 1) * self.rows:
             raise ValueError('actions tensor too small')
         o = self._outputs(out)
         stride = self.rows if per_step_actions else 0
-        check(self._lib.ce_multi_step_many(self._h, int(k), actions.data_ptr(), stride,
-                                           ctypes.byref(o)), 'ce_multi_step_many')
+        self._call('step_many', int(k), actions.data_ptr(), stride, ctypes.byref(o))
 
     def wait(self):
-        check(self._lib.ce_multi_wait(self._h), 'ce_multi_wait')
+        self._call('wait')
 
     def get_state(self):
         theta = np.zeros((self.num_envs, self.n_params), np.float32)
@@ -173,7 +176,7 @@ class MultiOptEngine:
 
     def close(self):
         if getattr(self, '_h', None):
-            self._lib.ce_multi_destroy(self._h)
+            self._fn('destroy')(self._h)
             self._h = None
 
     def __del__(self):
@@ -181,3 +184,92 @@ class MultiOptEngine:
             self.close()
         except Exception:
             pass
+
+
+# create_neural_net's default layers (custom_envs/utils/utils_tf.py:74) and
+# load_data's default set + batch size (custom_envs/data/load_data.py:47);
+# 'iris' is a git-LFS pointer in the reference, so its iris-shaped stand-in
+NN_DEFAULT_HIDDEN = (256, 256)
+NN_DEFAULT_DATA = 'iris_synthetic'
+
+
+def resolve_nn(data_set=None, hidden=None):
+    """(features float32 [N][F], labels int32 [N], K, batch size, hidden)."""
+    if data_set is None:
+        from custom_envs_amd.data import load_data
+        data_set = load_data(NN_DEFAULT_DATA, batch_size=32)
+    features = np.ascontiguousarray(data_set.features, dtype=np.float32)
+    targets = np.asarray(data_set.targets)
+    if features.ndim != 2 or targets.ndim != 2:
+        raise ValueError('the network problem needs (N, F) features and one-hot (N, K) targets')
+    labels = np.ascontiguousarray(np.argmax(targets, axis=1), dtype=np.int32)
+    hidden = tuple(int(h) for h in (NN_DEFAULT_HIDDEN if hidden is None else hidden))
+    return features, labels, targets.shape[1], int(data_set.batch_size), hidden
+
+
+class NNMultiEngine(MultiOptEngine):
+    """E MultiOptLRs envs over the OptimizeNN problem (get_problem('nn'),
+    custom_envs/problems/__init__.py:7-16): one agent per network parameter,
+    P = sum of the layers' kernel and bias sizes.  Seeds default to the env
+    index (the reference seeds each env from os.urandom, baseenvironment.py:17)."""
+
+    def __init__(self, num_envs, data_set=None, hidden=None, max_batches=400, max_history=5,
+                 device=0, auto_reset=True, seeds=None):
+        lib = _native.load()
+        features, labels, K, B, hidden = resolve_nn(data_set, hidden)
+        self.num_envs = int(num_envs)
+        self.max_history, self.max_batches = int(max_history), int(max_batches)
+        self.hidden, self.n_features, self.n_classes = hidden, features.shape[1], K
+        self.batch_size, self.n_rows = B, features.shape[0]
+        if len(hidden) > _native.CE_NN_MAX_HIDDEN:
+            raise _native.NativeEngineError('at most %d hidden layers' % _native.CE_NN_MAX_HIDDEN)
+        cfg = _native.CeNnConfig(abi_version=_native.ABI_VERSION, device=int(device),
+                                 num_envs=self.num_envs, n_rows=features.shape[0],
+                                 n_features=features.shape[1], n_classes=K, batch_size=B,
+                                 n_hidden=len(hidden), max_history=self.max_history,
+                                 max_batches=self.max_batches, auto_reset=1 if auto_reset else 0)
+        for i, w in enumerate(hidden):
+            cfg.hidden[i] = w
+        handle = ctypes.c_void_p()
+        check(lib.ce_nn_create(ctypes.byref(cfg), features.ctypes.data, labels.ctypes.data,
+                               ctypes.byref(handle)), 'ce_nn_create')
+        self._lib, self._h, self._prefix = lib, handle, 'ce_nn_'
+        self.n_params = int(lib.ce_nn_n_params(handle))
+        self._bind_outputs()
+        self.seed(seeds)
+
+    @property
+    def dims(self):
+        return (self.n_features,) + self.hidden + (self.n_classes,)
+
+    def seed(self, seeds=None):
+        """seeds[i] seeds env i as gym.utils.seeding.np_random(seeds[i])
+        (baseenvironment.py:20-28): the reset's initial weights and shuffle,
+        and the epoch-end shuffle."""
+        if seeds is None:
+            seeds = range(self.num_envs)
+        arr = np.ascontiguousarray([int(s) % (1 << 64) for s in seeds], dtype=np.uint64)
+        if arr.size != self.num_envs:
+            raise ValueError('one seed per env')
+        self._call('seed', arr.ctypes.data, int(arr.size))
+        return list(seeds)
+
+    def get_state(self):
+        E, P, N = self.num_envs, self.n_params, self.n_rows
+        st = {'theta': np.zeros((E, P), np.float32), 'gprev': np.zeros((E, P), np.float32),
+              'step': np.zeros(E, np.int32), 'cursor': np.zeros(E, np.int32),
+              'order': np.zeros((E, N), np.int32)}
+        self._call('get_state', *(st[k].ctypes.data for k in
+                                  ('theta', 'gprev', 'step', 'cursor', 'order')))
+        return st
+
+
+def create_engine(num_envs, problem='func', **kwargs):
+    """The engine a MultiOptLRs spec runs on: 'nn' -> NNMultiEngine, else the
+    function problems."""
+    if problem == 'nn':
+        kwargs.pop('initial_points', None)
+        return NNMultiEngine(num_envs, **kwargs)
+    kwargs.pop('data_set', None)
+    kwargs.pop('hidden', None)
+    return MultiOptEngine(num_envs, problem, **kwargs)

@@ -159,13 +159,13 @@ class OptVecEnv:
         request = _batch_request(environment_fns)
         self._engine = self._host = self.monitor = None
         if request is not None:
-            from custom_envs_amd.multi_engine import MultiOptEngine
+            from custom_envs_amd.multi_engine import create_engine
             from custom_envs_amd.utils.utils_logging import VecMonitor
             kwargs, mon, built = request
             for env in built:      # single-env engines the caller built eagerly
                 env.close()
             E = len(environment_fns)
-            self._engine = MultiOptEngine(E, **kwargs)
+            self._engine = create_engine(E, **kwargs)
             P, H = self._engine.n_params, self._engine.max_history
             self.agent_no_list = [P] * E
             self.observation_space = Box(low=-1e6, high=1e6, dtype=np.float32, shape=(3 * H,))

@@ -40,6 +40,21 @@
  *   ce_multi_step_async / ce_multi_wait / ce_multi_step_many / ce_multi_host_outputs /
  *   ce_multi_get_state / ce_multi_set_stream / ce_multi_destroy: as for Optimize-v0.
  *
+ * MultiOptLRs-v0 over the neural-network problem (get_problem('nn')):
+ *   ce_nn_create     MultiOptLRs.__init__(problem='nn')  multioptlrs.py:39-61
+ *                    + OptimizeNN.__init__        custom_envs/problems/optimize_nn.py:22-64
+ *                      (create_neural_net layers, custom_envs/utils/utils_tf.py:74-86)
+ *                    + OptVecEnv.__init__         optvecenv.py:57-68
+ *   ce_nn_seed       BaseEnvironment.seed         baseenvironment.py:20-28
+ *   ce_nn_seed_draws the reset's kernel init + shuffle and the epoch-end shuffle
+ *                    (optimize_nn.py:102-120 under use_random_state)
+ *   ce_nn_reset      OptVecEnv.reset -> MultiOptLRs.base_reset  multioptlrs.py:66-78
+ *   ce_nn_step       OptVecEnv.step -> MultiOptLRs.base_step    multioptlrs.py:80-129
+ *                    (+ OptimizeNN.get_gradient/get/next, optimize_nn.py:102-159)
+ *   ce_nn_step_async / ce_nn_wait / ce_nn_step_many / ce_nn_host_outputs /
+ *   ce_nn_get_state / ce_nn_set_stream / ce_nn_destroy / ce_nn_n_params:
+ *                    as for ce_multi_*.
+ *
  * Conventions
  *   - Every function returns CE_OK (0) or a negative ce_status; nothing
  *     throws across the ABI.  ce_last_error() returns a thread-local message.
@@ -230,6 +245,61 @@ int ce_multi_step_many(ce_multi_engine *eng, int32_t k, const float *actions,
 int ce_multi_host_outputs(ce_multi_engine *eng, ce_multi_outputs *view);
 /* theta [E][P] (problem parameters in agent order) and current_step [E] */
 int ce_multi_get_state(ce_multi_engine *eng, float *theta, int32_t *step);
+
+/* ------------------------------------------------------------------------
+ * MultiOptLRs-v0 over OptimizeNN: one agent per network parameter.  The
+ * network is F -> hidden[0] -> ... (relu) -> K (softmax), float32, flat
+ * parameters in Keras trainable_variables order [W1 | b1 | W2 | b2 | ...].
+ * Rows and outputs as for ce_multi_* (ce_multi_outputs).
+ */
+typedef struct ce_nn_engine ce_nn_engine;
+
+#define CE_NN_MAX_HIDDEN 4
+
+typedef struct ce_nn_config {
+    int32_t abi_version;
+    int32_t device;
+    int32_t num_envs;      /* E                                                 */
+    int32_t n_rows;        /* N dataset rows                                    */
+    int32_t n_features;    /* F                                                 */
+    int32_t n_classes;     /* K (<= 32)                                         */
+    int32_t batch_size;    /* B rows per batch (load_data default 32; <= 32)    */
+    int32_t n_hidden;      /* hidden layers, 1..CE_NN_MAX_HIDDEN                */
+    int32_t hidden[CE_NN_MAX_HIDDEN]; /* units per hidden layer (multiples of 32,
+                              <= 512); create_neural_net default (256, 256)    */
+    int32_t max_history;   /* H (<= 16)                                         */
+    int32_t max_batches;   /* episode length (default 400)                      */
+    int32_t auto_reset;    /* 1: OptVecEnv auto-reset; 0: single env            */
+} ce_nn_config;
+
+int ce_nn_create(const ce_nn_config *cfg, const float *features /* [N][F] */,
+                 const int32_t *labels /* [N] class index */, ce_nn_engine **out);
+void ce_nn_destroy(ce_nn_engine *eng);
+int ce_nn_set_stream(ce_nn_engine *eng, void *hip_stream);
+/* P: parameters (= agents) per env */
+int ce_nn_n_params(const ce_nn_engine *eng);
+/* seeds[i] seeds env i as gym.utils.seeding.np_random(seeds[i]); must precede
+   the first reset */
+int ce_nn_seed(ce_nn_engine *eng, const uint64_t *seeds, int32_t n);
+/* Host-only: the float32 initial parameters [P], the reset shuffle [N] and
+   the epoch-end shuffle [N] of a seed (any output may be NULL).  No GPU. */
+int ce_nn_seed_draws(uint64_t seed, int32_t n_dims, const int32_t *dims /* F, hidden..., K */,
+                     int32_t n_rows, float *init_weights, int32_t *reset_perm,
+                     int32_t *epoch_perm);
+int ce_nn_reset(ce_nn_engine *eng, const ce_multi_outputs *out, uint32_t flags);
+int ce_nn_step(ce_nn_engine *eng, const float *actions /* [E*P] rows */,
+               const ce_multi_outputs *out, uint32_t flags);
+int ce_nn_step_async(ce_nn_engine *eng, const float *actions, const ce_multi_outputs *out,
+                     uint32_t flags);
+int ce_nn_wait(ce_nn_engine *eng);
+int ce_nn_step_many(ce_nn_engine *eng, int32_t k, const float *actions,
+                    int64_t action_step_stride, const ce_multi_outputs *out);
+int ce_nn_host_outputs(ce_nn_engine *eng, ce_multi_outputs *view);
+/* theta [E][P] (agent order), gprev [E][P] (newest raw-history gradient),
+   step [E], cursor [E] (batch index in the epoch), order [E][N] (dataset row
+   of each current row); any pointer may be NULL */
+int ce_nn_get_state(ce_nn_engine *eng, float *theta, float *gprev, int32_t *step,
+                    int32_t *cursor, int32_t *order);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,250 @@
+"""MultiOptLRs over OptimizeNN: the HIP engine (ce_nn_*) against the oracle.
+
+Two kinds of check, because the observation is a ratio of consecutive
+gradients (g_t / |g_{t-1}|, utils_env.py:155-161) and a near-zero gradient
+entry turns float32 summation-order noise into an arbitrary ratio:
+
+* state parity with the live oracle (oracle/multinn.py), float32 network
+  arithmetic in a different summation order:
+    exact      done flags, episode lengths, the composed row order
+               (reset + epoch-end shuffles), theta at every reset;
+    1e-4       theta and the newest gradient, relative to max |.| of the
+               env's vector; batch loss and reward relative;
+* formula parity on the engine's own state: every observation entry, the
+  loss ratio, and the info statistics recomputed in numpy from the engine's
+  theta / gradient / loss sequence with the reference's formulas
+  (multioptlrs.py:90-127), to float32 rounding of the float64 result.
+"""
+import numpy as np
+import pytest
+
+from oracle.multinn import MultiOptLRsNN, nn_draws
+
+pytestmark = pytest.mark.gpu
+
+BOUNDS = 100.0
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a ROCm device (run under gpurun)')
+
+
+def _iris():
+    from custom_envs_amd.data import load_data
+    return load_data('iris_synthetic', batch_size=32)
+
+
+def _ratio(a, b):
+    with np.errstate(divide='ignore', invalid='ignore'):
+        return np.nan_to_num(np.asarray(a, np.float64) / np.abs(np.asarray(b, np.float64)))
+
+
+def _obs_form(x):
+    return (np.clip(np.nan_to_num(x), -BOUNDS, BOUNDS) - 1).astype(np.float32)
+
+
+def _run_engine(ds, hidden, seeds, acts, max_batches, H=5):
+    from custom_envs_amd.multi_engine import NNMultiEngine
+    E = len(seeds)
+    eng = NNMultiEngine(E, data_set=ds, hidden=hidden, max_batches=max_batches,
+                        max_history=H, seeds=seeds)
+    P = eng.n_params
+    rec = {'obs0': eng.reset().reshape(E, P, 3 * H), 'state0': eng.get_state(), 'steps': []}
+    for t in range(acts.shape[0]):
+        out = eng.step(acts[t])
+        rec['steps'].append({
+            'obs': out['obs'].reshape(E, P, 3 * H).copy(),
+            'reward': out['reward'].reshape(E, P).copy(),
+            'done': out['done'].reshape(E, P).copy(),
+            'info': out['info'].copy(),
+            'len': out['episode_len'].copy(),
+            'state': eng.get_state()})
+    rows = np.asarray(eng.row_agents)
+    eng.close()
+    return P, rows, rec
+
+
+def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state_tol=1e-4):
+    """acts_env: [T][P] actions in row order for env i."""
+    P = rows.size
+    agent_row = np.empty(P, np.int64)
+    agent_row[rows] = np.arange(P)
+    env = MultiOptLRsNN(ds.features, ds.targets, hidden=hidden, batch_size=32,
+                        max_batches=max_batches, max_history=H)
+    env.seed(seed)
+    env.reset()
+    th0 = nn_draws(seed, env.model.dims, len(ds.features))[0]
+    assert np.array_equal(rec['state0']['theta'][i], th0)
+    assert np.all(rec['obs0'][i] == -1.0)
+    names = env.names
+    theta_prev = th0.astype(np.float64)
+    g_prev = None           # engine gradient of the previous step (None after a reset)
+    l_prev = None
+    ring = []               # engine's age-0 obs entries of earlier steps this episode
+    for t in range(acts_env.shape[0]):
+        step = rec['steps'][t]
+        act_rows = acts_env[t]
+        obs_o, rew_o, done_o, info_o = env.step({names[p]: act_rows[agent_row[p]]
+                                                 for p in range(P)})
+        # ---- exact: done, episode length, row order
+        assert bool(step['done'][i, 0]) == done_o and np.all(step['done'][i] == step['done'][i, 0])
+        assert step['len'][i] == info_o['episode']['l']
+        st = step['state']
+        loss = float(step['info'][i, 1])
+        # ---- state parity (float32 network arithmetic, different order)
+        th_o = env.model.params
+        g_o = env.history['gradients'][0]
+        th_e = theta_after = None
+        if not done_o:
+            th_e = st['theta'][i]
+            np.testing.assert_allclose(th_e, th_o, rtol=0,
+                                       atol=state_tol * max(np.abs(th_o).max(), 1e-30))
+            assert np.array_equal(st['order'][i], env.order()), t
+            theta_after = th_e.astype(np.float64)
+        g_e = st['gprev'][i]
+        np.testing.assert_allclose(g_e, g_o, rtol=0, atol=state_tol * np.abs(g_o).max() + 1e-7)
+        assert loss == pytest.approx(float(info_o['batch_loss']), rel=state_tol)
+        assert step['reward'][i, 0] == pytest.approx(float(rew_o), rel=state_tol, abs=state_tol)
+        # ---- formula parity on the engine's own sequence
+        obs = step['obs'][i][agent_row]            # agent order, [P][3H]
+        if done_o:
+            # auto-reset: the reset observation, theta back at theta0
+            assert np.all(obs == -1.0)
+            assert np.array_equal(st['theta'][i], th0)
+            env.reset()
+            assert np.array_equal(st['order'][i], env.order()), t
+            theta_prev, g_prev, l_prev, ring = th0.astype(np.float64), None, None, []
+            continue
+        w_new = _obs_form(_ratio(theta_after, theta_prev))
+        assert np.array_equal(obs[:, 0], w_new), t
+        if g_prev is not None:
+            g_new = _obs_form(_ratio(g_e, g_prev))
+            assert np.array_equal(obs[:, 2 * H], g_new), t
+            assert float(step['info'][i, 12]) == pytest.approx(
+                np.mean(np.abs(_ratio(g_e, g_prev))), rel=1e-5)
+            assert float(step['info'][i, 13]) == pytest.approx(
+                np.mean(np.abs(g_e.astype(np.float64) - g_prev)), rel=1e-5, abs=1e-12)
+        if l_prev is not None:
+            adj_l = float(_ratio(loss, l_prev))
+            assert float(step['info'][i, 11]) == pytest.approx(adj_l, rel=1e-6)
+            assert np.all(obs[:, H] == _obs_form(adj_l))
+        for k, old in enumerate(reversed(ring[-(H - 1):]), start=1):
+            assert np.array_equal(obs[:, k], old[:, 0]), (t, k)
+            assert np.array_equal(obs[:, 2 * H + k], old[:, 2 * H]), (t, k)
+            assert np.all(obs[:, H + k] == old[0, H])
+        for k in range(len(ring) + 1, H):
+            assert np.all(obs[:, k] == -1.0) and np.all(obs[:, 2 * H + k] == -1.0)
+        wsum = np.abs(theta_after).sum()
+        assert float(step['info'][i, 3]) == pytest.approx(wsum, rel=1e-6)
+        lr = (10.0 ** (act_rows[agent_row].astype(np.float32) - np.float32(4)).astype(np.float64)
+              ).astype(np.float32).astype(np.float64)
+        assert float(step['info'][i, 4]) == pytest.approx(lr.mean(), rel=1e-6)
+        assert float(step['info'][i, 5]) == pytest.approx(lr.std(), rel=1e-4, abs=1e-9)
+        assert float(step['info'][i, 10]) == pytest.approx(float(info_o['loss_mean']),
+                                                           rel=state_tol)
+        ring.append(obs.copy())
+        theta_prev, g_prev, l_prev = theta_after, g_e.astype(np.float64), loss
+
+
+def _actions(T, E, P, lo, hi, seed):
+    return np.random.RandomState(seed).uniform(lo, hi, (T, E * P)).astype(np.float32)
+
+
+@pytest.mark.parametrize('hidden', [(64,), (96, 32), (32, 64, 128)])
+def test_small_networks_against_oracle(hidden):
+    """max_batches 7 over 16 steps: two auto-resets, epochs of 5 batches
+    (the ragged 22-row batch), split-k forwards (widths < 256)."""
+    ds = _iris()
+    seeds = [5, 17, 2**33 + 1]
+    from custom_envs_amd.multi_engine import NNMultiEngine
+    probe = NNMultiEngine(1, data_set=ds, hidden=hidden)
+    P = probe.n_params
+    probe.close()
+    acts = _actions(16, len(seeds), P, 1.0, 2.5, 3)
+    P, rows, rec = _run_engine(ds, hidden, seeds, acts, max_batches=7)
+    for i, seed in enumerate(seeds):
+        _check_env(ds, hidden, seed, acts[:, i * P:(i + 1) * P], rows, rec, i, 7)
+
+
+def test_default_network_against_oracle():
+    """get_problem('nn') defaults: create_neural_net (256, 256) over the
+    iris-shaped set, P = 67,843 agents per env."""
+    ds = _iris()
+    seeds = [0, 9]
+    hidden = (256, 256)
+    P = 4 * 256 + 256 + 256 * 256 + 256 + 256 * 3 + 3
+    acts = _actions(6, len(seeds), P, 1.0, 2.5, 4)
+    P2, rows, rec = _run_engine(ds, hidden, seeds, acts, max_batches=400)
+    assert P2 == P
+    for i, seed in enumerate(seeds):
+        _check_env(ds, hidden, seed, acts[:, i * P:(i + 1) * P], rows, rec, i, 400)
+
+
+def test_divergence_stops_early_with_penalty():
+    """multioptlrs.py:105-107: loss > 1e4 ends the episode with reward
+    reduced by (max_batches - step); lr 1e2..1e4 drives the loss there."""
+    ds = _iris()
+    from custom_envs_amd.multi_engine import NNMultiEngine
+    hidden = (64,)
+    eng = NNMultiEngine(2, data_set=ds, hidden=hidden, max_batches=50, seeds=[1, 2])
+    P = eng.n_params
+    eng.reset()
+    acts = _actions(12, 2, P, 6.0, 8.0, 5)
+    oracles = []
+    for seed in (1, 2):
+        env = MultiOptLRsNN(ds.features, ds.targets, hidden=hidden, max_batches=50)
+        env.seed(seed)
+        env.reset()
+        oracles.append(env)
+    rows = np.asarray(eng.row_agents)
+    agent_row = np.empty(P, np.int64)
+    agent_row[rows] = np.arange(P)
+    early = 0
+    for t in range(12):
+        out = eng.step(acts[t])
+        for i, env in enumerate(oracles):
+            a = acts[t, i * P:(i + 1) * P]
+            _, rew, done, info = env.step({env.names[p]: a[agent_row[p]] for p in range(P)})
+            assert bool(out['done'][i * P]) == done
+            assert out['episode_len'][i] == info['episode']['l']
+            if done:
+                early += info['episode']['l'] < 50
+                if np.isfinite(rew):
+                    assert out['reward'][i * P] == pytest.approx(float(rew), rel=1e-3, abs=1e-3)
+                env.reset()
+    eng.close()
+    assert early > 0
+
+
+def test_optvecenv_and_single_env_surface():
+    """OptVecEnv over make('MultiOptLRs-v0', problem='nn', ...) runs on one
+    engine; rows are env-major in sorted agent-name order; the single env
+    returns the reference's Dict surface."""
+    import functools
+    import custom_envs_amd
+    from custom_envs_amd.vectorize.optvecenv import OptVecEnv
+    ds = _iris()
+    fn = functools.partial(custom_envs_amd.make, 'MultiOptLRs-v0', problem='nn',
+                           data_set=ds, hidden=(32,), max_batches=5)
+    venv = OptVecEnv([fn] * 3)
+    assert venv.engine_backed
+    P = 4 * 32 + 32 + 32 * 3 + 3
+    assert venv.num_envs == 3 * P and venv.agent_no_list == [P] * 3
+    obs = venv.reset()
+    assert obs.shape == (3 * P, 15) and np.all(obs == -1)
+    for t in range(6):
+        states, rewards, terminals, infos = venv.step(np.full(3 * P, 1.5, np.float32))
+        assert states.shape == (3 * P, 15) and len(infos) == 3 * P
+        assert np.all(terminals == (t == 4))
+    venv.close()
+    env = custom_envs_amd.make('MultiOptLRs-v0', problem='nn', data_set=ds, hidden=(32,))
+    env.seed(3)
+    state = env.reset()
+    assert len(state) == P and all(np.all(v == -1) for v in state.values())
+    state, reward, terminal, info = env.step({n: np.float32(1.5) for n in state})
+    assert isinstance(reward, float) and isinstance(terminal, bool)
+    assert info['loss'] is None and set(info) >= {'batch_loss', 'grads_mean', 'episode'}
+    env.close()
