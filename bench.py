@@ -40,6 +40,8 @@ METRIC_MULTI = ('vectorised env-steps/sec, MultiOptLRs-v0 (4 agents) via OptVecE
                 'config 5, MI355X vs host CPU')
 METRIC_MLP = ('vectorised env-steps/sec, Optimize-v0 over the 784-64-10 MLP @4096 envs, '
               'config 3, MI355X vs host CPU')
+METRIC_NN = ('vectorised env-steps/sec, MultiOptLRs-v0 over the OptimizeNN (256, 256) network '
+             'via OptVecEnv, one agent per parameter, 1/2/4/8 MI355X vs host CPU')
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 F64_VALU_PEAK_TFLOPS = 78.6
@@ -83,6 +85,23 @@ def mlp_train_bytes(P):
     return 4 * P + 8 * P + 16 * P + 4 * (2 * P + 1) + 16 + 8 + 9
 
 
+def nn_bytes_per_env_step(P, H=5):
+    """Algorithmic HBM bytes per env-step of MultiOptLRs over the network
+    (the job's own traffic, not the engine's): theta read and
+    theta' written 8P, actions 4P, the previous gradient read and the new
+    one written 8P, the adjusted w~/g~ rings read 8(H-1)P and written 8P,
+    obs rows 4*3H*P, reward 4P and done P."""
+    return 8 * P + 4 * P + 8 * P + 8 * (H - 1) * P + 8 * P + 12 * H * P + 5 * P
+
+
+def nn_flops_per_env_step(dims):
+    """MFMA/VALU FLOPs of two forward+backward passes on a 32-row batch:
+    forward 2B sum(d_l d_l+1), dW 2B sum(d_l d_l+1), dH 2B sum_{l>0}(d_l d_l+1)."""
+    pairs = [a * b for a, b in zip(dims[:-1], dims[1:])]
+    one = 2 * 32 * (2 * sum(pairs) + sum(pairs[1:]))
+    return 2 * one
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
@@ -90,7 +109,7 @@ def parse():
     p.add_argument('--warmup', type=int, default=200)
     p.add_argument('--envs', type=int, default=None,
                    help='envs per GPU (default 4096 optimize, 1024 multi)')
-    p.add_argument('--workload', default='optimize', choices=['optimize', 'multi', 'mlp'])
+    p.add_argument('--workload', default='optimize', choices=['optimize', 'multi', 'mlp', 'nn'])
     p.add_argument('--precision', default='f64', choices=['f64', 'f32'])
     p.add_argument('--graph-steps', type=int, default=250, help='steps per hipGraph replay')
     p.add_argument('--gather', action='store_true', help='all-gather outputs every step')
@@ -100,7 +119,7 @@ def parse():
                    help='run the timed steps only (for rocprofv3)')
     args = p.parse_args()
     if args.envs is None:
-        args.envs = 1024 if args.workload == 'multi' else 4096
+        args.envs = {'multi': 1024, 'nn': 1024}.get(args.workload, 4096)
     return args
 
 
@@ -248,6 +267,44 @@ def build_multi(args, torch, device, rank, world):
     return eng, actions, S
 
 
+def build_nn(args, torch, device, rank, world):
+    from custom_envs_amd.multi_engine import NNMultiEngine
+    E = args.envs
+    eng = NNMultiEngine(E, max_batches=400, max_history=5, device=device,
+                        seeds=[rank * E + i for i in range(E)])
+    gen = torch.Generator(device='cuda').manual_seed(11 + rank)
+    S = 2                                 # two action blocks of [E*P] rows
+    actions = torch.rand((S, E * eng.n_params), generator=gen, device='cuda') * 1.5 + 1.0
+    return eng, actions, S
+
+
+def cpu_baseline_nn(budget_s):
+    """The reference's path restated: OptVecEnv (ThreadVecEnv of OptEnvRunner)
+    over the numpy oracle MultiOptLRs with the OptimizeNN (256, 256) problem."""
+    from custom_envs_amd.data import load_data
+    from oracle.multioptlrs import OptVecEnv
+    from oracle.multinn import MultiOptLRsNN
+    ds = load_data('iris_synthetic', batch_size=32)
+    n = 2
+
+    def make(seed):
+        def build():
+            env = MultiOptLRsNN(ds.features, ds.targets, hidden=(256, 256), max_batches=400)
+            env.seed(seed)
+            return env
+        return build
+    venv = OptVecEnv([make(i) for i in range(n)])
+    venv.reset()
+    acts = np.random.RandomState(11).uniform(1, 2.5, (venv.num_envs, 1)).astype(np.float32)
+    steps, wall, cpu = _time_cpu(venv, acts, budget_s)
+    venv.close()
+    return {'value': n * steps / wall, 'unit': 'env-steps/s',
+            'cores': max(1, int(round(cpu / wall))), 'kind': 'port',
+            'sample': '%d envs x 67843 agents x %d steps of OptVecEnv over ThreadVecEnv around '
+                      'the numpy oracle MultiOptLRs(problem=nn); %.1f s wall, %.1f s CPU; '
+                      'os.cpu_count()=%d' % (n, steps, wall, cpu, os.cpu_count())}
+
+
 def main():
     args = parse()
     import torch
@@ -264,7 +321,9 @@ def main():
     device = torch.cuda.current_device()
     multi = args.workload == 'multi'
     mlp = args.workload == 'mlp'
-    builder = {'optimize': build_optimize, 'multi': build_multi, 'mlp': build_mlp}[args.workload]
+    nn = args.workload == 'nn'
+    builder = {'optimize': build_optimize, 'multi': build_multi, 'mlp': build_mlp,
+               'nn': build_nn}[args.workload]
     eng, actions, S = builder(args, torch, device, rank, world)
     E = args.envs
     stream = torch.cuda.Stream()          # a real stream: graphs cannot capture the null stream
@@ -355,7 +414,9 @@ def main():
         host_rate = host_loop_rate(args, device, E)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if multi:
+        if nn:
+            cpu = cpu_baseline_nn(args.cpu_seconds)
+        elif multi:
             cpu = cpu_baseline_multi(E, args.cpu_seconds)
         elif mlp:
             cpu = cpu_baseline_mlp(E, args.cpu_seconds)
@@ -366,6 +427,8 @@ def main():
         if mlp:
             line = mlp_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard,
                             phase_ms)
+        elif nn:
+            line = nn_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard)
         else:
             line = (multi_line if multi else optimize_line)(args, eng, world, E, S, elapsed,
                                                             kernel_ms, kernel_ms_mean, shard)
@@ -489,6 +552,42 @@ def multi_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard
             'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
             'kernel_ms_mean': kernel_ms_mean,
             'kernel': 'ce::multi_step_kernel<4>',
+        },
+    })
+    return line
+
+
+def nn_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
+    P, H = eng.n_params, eng.max_history
+    bpe = nn_bytes_per_env_step(P, H)
+    flops = nn_flops_per_env_step(eng.dims)
+    achieved = bpe * E / (kernel_ms * 1e-3) / 1e9
+    line = {'metric': METRIC_NN}
+    line.update(_common(args, world, E, S, elapsed, shard))
+    line.update({
+        'agent_steps_per_s': P * world * E * args.steps / elapsed,
+        'dtype': 'f32',
+        'data': 'synthetic: iris-shaped 150 x 4, 3 classes (load_data default stand-in), '
+                'batches of 32; glorot-uniform init per env seed; actions uniform(1, 2.5) '
+                'float32 generated on device (lr 1e-3..3e-2)',
+        'config': {
+            'workload': 'MultiOptLRs-v0(problem=nn) x OptVecEnv: network 4-256-256-3 '
+                        '(P=%d agents per env), H=5, max_batches=400, %d envs per GPU, '
+                        'minibatch cycling with on-device reshuffle, in-kernel auto-reset, '
+                        'device-resident actions/outputs' % (P, E),
+            'envs_per_gpu': E, 'global_envs': world * E, 'agents': P, 'hidden': list(eng.hidden),
+            'parallelism': 'env-sharded x%d (no collective)' % world,
+        },
+        'roofline': {
+            'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+            'kernel': 'one step = ce::nn_grad_kernel, nn_update_kernel, nn_step_kernel, '
+                      'nn_agent_kernel (dominant), nn_finalize_kernel',
+            'bytes_per_env_step': bpe,
+            'step_ms_median': kernel_ms, 'step_ms_mean': kernel_ms_mean,
+            'flops_per_env_step': flops,
+            'mfma_tflops': flops * E / (kernel_ms * 1e-3) / 1e12,
+            'mfma_peak_tflops': MFMA_F32_PEAK_TFLOPS,
         },
     })
     return line

@@ -25,9 +25,12 @@ struct ce_nn_engine {
     hipStream_t own_stream = nullptr, stream = nullptr;
     float *X = nullptr;
     int32_t *label = nullptr;
-    float *theta = nullptr, *theta_n = nullptr, *theta0 = nullptr, *gprev = nullptr;
+    float *theta_buf[2] = {nullptr, nullptr}, *g_buf[2] = {nullptr, nullptr};
+    int parity = 0;                    // theta_buf[parity], g_buf[parity] are current
+    float *theta0 = nullptr, *gU = nullptr, *loss_b = nullptr;
     float *rw = nullptr, *rg = nullptr, *hl = nullptr;
-    double *al = nullptr, *sw = nullptr, *sg = nullptr, *hsg = nullptr, *lr_stats = nullptr;
+    double *al = nullptr, *sw = nullptr, *sg = nullptr, *hsg = nullptr;
+    double *part_u = nullptr, *part_c = nullptr;
     int32_t *step = nullptr, *cursor = nullptr, *order = nullptr, *order_sel = nullptr;
     int32_t *reset_perm = nullptr, *epoch_perm = nullptr, *agent_row = nullptr;
     float *d_act = nullptr, *h_act = nullptr;
@@ -36,7 +39,7 @@ struct ce_nn_engine {
     char *d_out = nullptr, *h_out = nullptr;
     bool seeded = false, was_reset = false;
     hipGraphExec_t graph = nullptr;
-    int graph_k = 0;
+    int graph_k = 0, graph_parity = 0;
     const float *graph_act = nullptr;
     int64_t graph_stride = 0;
     ce_multi_outputs graph_out{};
@@ -61,6 +64,10 @@ ce_multi_outputs region(const ce_nn_engine *e, char *base) {
 
 ce::NnArgs make_args(const ce_nn_engine *e, const float *act, const ce_multi_outputs &o) {
     ce::NnArgs a = e->base;
+    a.theta = e->theta_buf[e->parity];
+    a.theta_n = e->theta_buf[1 - e->parity];
+    a.gprev = e->g_buf[e->parity];
+    a.gN = e->g_buf[1 - e->parity];
     a.act = act;
     a.obs = o.obs;
     a.reward = o.reward;
@@ -74,9 +81,16 @@ bool complete(const ce_multi_outputs *o) {
     return o && o->obs && o->reward && o->done && o->info && o->episode_len;
 }
 
-void launch_step(const ce_nn_engine *e, const ce::NnArgs &a, hipStream_t s) {
+// one step's five launches; the ping-pong pairs swap afterwards
+void launch_step(ce_nn_engine *e, const float *act, const ce_multi_outputs &o, hipStream_t s) {
+    const ce::NnArgs a = make_args(e, act, o);
+    const size_t stage = static_cast<size_t>(ce::kNnChunk) * 3 * a.H * sizeof(float);
     hipLaunchKernelGGL(ce::nn_grad_kernel, dim3(a.E), dim3(ce::kNnBlock), a.lds_bytes, s, a);
+    hipLaunchKernelGGL(ce::nn_update_kernel, dim3(a.nchunk_u, a.E), dim3(ce::kNnChunk), 0, s, a);
     hipLaunchKernelGGL(ce::nn_step_kernel, dim3(a.E), dim3(ce::kNnBlock), a.lds_bytes, s, a);
+    hipLaunchKernelGGL(ce::nn_agent_kernel, dim3(a.nchunk, a.E), dim3(ce::kNnChunk), stage, s, a);
+    hipLaunchKernelGGL(ce::nn_finalize_kernel, dim3(a.E), dim3(ce::kNnChunk), 0, s, a);
+    e->parity ^= 1;
 }
 
 void copy_out(const ce_nn_engine *e, const ce_multi_outputs &src, const ce_multi_outputs *dst) {
@@ -98,7 +112,7 @@ int do_step(ce_nn_engine *e, const float *actions, const ce_multi_outputs *out, 
     if (flags & CE_PTR_DEVICE) {
         if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
         const ce_multi_outputs o = out ? *out : region(e, e->d_out);
-        launch_step(e, make_args(e, actions, o), e->stream);
+        launch_step(e, actions, o, e->stream);
         CE_HIP(hipGetLastError());
         if (sync) CE_HIP(hipStreamSynchronize(e->stream));
         return CE_OK;
@@ -106,7 +120,7 @@ int do_step(ce_nn_engine *e, const float *actions, const ce_multi_outputs *out, 
     std::memcpy(e->h_act, actions, rows * sizeof(float));
     CE_HIP(hipMemcpyAsync(e->d_act, e->h_act, rows * sizeof(float), hipMemcpyHostToDevice,
                           e->stream));
-    launch_step(e, make_args(e, e->d_act, region(e, e->d_out)), e->stream);
+    launch_step(e, e->d_act, region(e, e->d_out), e->stream);
     CE_HIP(hipGetLastError());
     CE_HIP(hipMemcpyAsync(e->h_out, e->d_out, e->out_bytes, hipMemcpyDeviceToHost, e->stream));
     if (sync) {
@@ -137,6 +151,7 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
         return fail(CE_EUNSUPPORTED, "ce_nn_create: 2..32 classes");
     if (cfg->batch_size <= 0 || cfg->batch_size > ce::kNnBatch)
         return fail(CE_EUNSUPPORTED, "ce_nn_create: batch_size must be 1..32");
+    if (cfg->num_envs > 65535) return fail(CE_EUNSUPPORTED, "ce_nn_create: at most 65535 envs");
     if (cfg->max_history <= 0 || cfg->max_history > ce::kNnMaxH)
         return fail(CE_EUNSUPPORTED, "ce_nn_create: max_history must be 1..16");
     if (cfg->n_features > 1024) return fail(CE_EUNSUPPORTED, "ce_nn_create: n_features <= 1024");
@@ -182,6 +197,9 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     e->P = a.P = static_cast<int>(P);
     e->Ps = static_cast<size_t>((P + 63) & ~63L);
     a.Ps = static_cast<int>(e->Ps);
+    a.nchunk = static_cast<int>((P + ce::kNnChunk - 1) / ce::kNnChunk);
+    a.nchunk_u = static_cast<int>((P + ce::kNnChunk * ce::kNnUpdPer - 1) /
+                                  (ce::kNnChunk * ce::kNnUpdPer));
     // LDS: X, every hidden activation, the logits, the split-k scratch
     int fl = 0;
     a.lds_x = fl;
@@ -194,6 +212,8 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     }
     a.lds_z = fl;
     fl += ce::kNnBatch * host_ld(a.K);
+    a.lds_wo = fl;
+    fl += (a.dims[L] * a.K + 3) & ~3;
     a.lds_part = fl;
     if (a.split) fl += ce::kNnWaves * 32 * 32;
     a.lds_bytes = fl * static_cast<int>(sizeof(float));
@@ -213,10 +233,17 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
     CE_TRY(hipMemcpy(e->X, features, N * a.F * sizeof(float), hipMemcpyHostToDevice));
     CE_TRY(hipMemcpy(e->label, labels, N * sizeof(int32_t), hipMemcpyHostToDevice));
-    CE_TRY(hipMalloc(&e->theta, E * Ps * sizeof(float)));
-    CE_TRY(hipMalloc(&e->theta_n, E * Ps * sizeof(float)));
+    for (int i = 0; i < 2; ++i) {
+        CE_TRY(hipMalloc(&e->theta_buf[i], E * Ps * sizeof(float)));
+        CE_TRY(hipMalloc(&e->g_buf[i], E * Ps * sizeof(float)));
+        CE_TRY(hipMemset(e->theta_buf[i], 0, E * Ps * sizeof(float)));
+        CE_TRY(hipMemset(e->g_buf[i], 0, E * Ps * sizeof(float)));
+    }
     CE_TRY(hipMalloc(&e->theta0, E * Ps * sizeof(float)));
-    CE_TRY(hipMalloc(&e->gprev, E * Ps * sizeof(float)));
+    CE_TRY(hipMalloc(&e->gU, E * Ps * sizeof(float)));
+    CE_TRY(hipMalloc(&e->loss_b, E * sizeof(float)));
+    CE_TRY(hipMalloc(&e->part_u, E * a.nchunk_u * 3 * sizeof(double)));
+    CE_TRY(hipMalloc(&e->part_c, E * a.nchunk * 5 * sizeof(double)));
     CE_TRY(hipMalloc(&e->rw, H * E * Ps * sizeof(float)));
     CE_TRY(hipMalloc(&e->rg, H * E * Ps * sizeof(float)));
     CE_TRY(hipMalloc(&e->al, H * E * sizeof(double)));
@@ -224,7 +251,6 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     CE_TRY(hipMalloc(&e->sg, H * E * sizeof(double)));
     CE_TRY(hipMalloc(&e->hl, ce::kRawHist * E * sizeof(float)));
     CE_TRY(hipMalloc(&e->hsg, ce::kRawHist * E * sizeof(double)));
-    CE_TRY(hipMalloc(&e->lr_stats, 2 * E * sizeof(double)));
     CE_TRY(hipMalloc(&e->step, E * sizeof(int32_t)));
     CE_TRY(hipMalloc(&e->cursor, E * sizeof(int32_t)));
     CE_TRY(hipMalloc(&e->order, 2 * E * N * sizeof(int32_t)));
@@ -237,9 +263,6 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     CE_TRY(hipMemset(e->step, 0, E * sizeof(int32_t)));
     CE_TRY(hipMemset(e->cursor, 0, E * sizeof(int32_t)));
     CE_TRY(hipMemset(e->order_sel, 0, E * sizeof(int32_t)));
-    CE_TRY(hipMemset(e->gprev, 0, E * Ps * sizeof(float)));
-    CE_TRY(hipMemset(e->theta, 0, E * Ps * sizeof(float)));
-    CE_TRY(hipMemset(e->theta_n, 0, E * Ps * sizeof(float)));
     {
         // the dataset object starts in file order (the construction-time
         // shuffle draws from the unseeded global npr, optimize_nn.py:64,
@@ -275,10 +298,11 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
 #undef CE_TRY
     a.X = e->X;
     a.label = e->label;
-    a.theta = e->theta;
-    a.theta_n = e->theta_n;
     a.theta0 = e->theta0;
-    a.gprev = e->gprev;
+    a.gU = e->gU;
+    a.loss_b = e->loss_b;
+    a.part_u = e->part_u;
+    a.part_c = e->part_c;
     a.rw = e->rw;
     a.rg = e->rg;
     a.al = e->al;
@@ -286,7 +310,6 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     a.sg = e->sg;
     a.hl = e->hl;
     a.hsg = e->hsg;
-    a.lr_stats = e->lr_stats;
     a.step = e->step;
     a.cursor = e->cursor;
     a.order = e->order;
@@ -302,8 +325,9 @@ void ce_nn_destroy(ce_nn_engine *e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->graph) (void)hipGraphExecDestroy(e->graph);
-    void *dev[] = {e->X, e->label, e->theta, e->theta_n, e->theta0, e->gprev, e->rw, e->rg,
-                   e->al, e->sw, e->sg, e->hl, e->hsg, e->lr_stats, e->step, e->cursor,
+    void *dev[] = {e->X, e->label, e->theta_buf[0], e->theta_buf[1], e->g_buf[0], e->g_buf[1],
+                   e->theta0, e->gU, e->loss_b, e->part_u, e->part_c, e->rw, e->rg,
+                   e->al, e->sw, e->sg, e->hl, e->hsg, e->step, e->cursor,
                    e->order, e->order_sel, e->reset_perm, e->epoch_perm, e->agent_row,
                    e->d_act, e->d_out};
     for (void *p : dev)
@@ -400,9 +424,11 @@ int ce_nn_step_many(ce_nn_engine *e, int32_t k, const float *actions, int64_t st
     if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "bad arguments");
     if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
     const ce_multi_outputs o = out ? *out : region(e, e->d_out);
+    // the captured launches bake in the ping-pong pointers of their parity
+    const int p0 = e->parity;
     const bool hit = e->graph && e->graph_k == k && e->graph_act == actions &&
                      e->graph_stride == stride && e->graph_stream == e->stream &&
-                     std::memcmp(&e->graph_out, &o, sizeof(o)) == 0;
+                     e->graph_parity == p0 && std::memcmp(&e->graph_out, &o, sizeof(o)) == 0;
     if (!hit) {
         if (e->graph) {
             CE_HIP(hipGraphExecDestroy(e->graph));
@@ -410,7 +436,8 @@ int ce_nn_step_many(ce_nn_engine *e, int32_t k, const float *actions, int64_t st
         }
         hipGraph_t g;
         CE_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-        for (int s = 0; s < k; ++s) launch_step(e, make_args(e, actions + s * stride, o), e->stream);
+        for (int s = 0; s < k; ++s) launch_step(e, actions + s * stride, o, e->stream);
+        e->parity = p0;
         CE_HIP(hipStreamEndCapture(e->stream, &g));
         hipError_t err = hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0);
         (void)hipGraphDestroy(g);
@@ -421,8 +448,10 @@ int ce_nn_step_many(ce_nn_engine *e, int32_t k, const float *actions, int64_t st
         e->graph_stride = stride;
         e->graph_out = o;
         e->graph_stream = e->stream;
+        e->graph_parity = p0;
     }
     CE_HIP(hipGraphLaunch(e->graph, e->stream));
+    e->parity = p0 ^ (k & 1);
     return CE_OK;
 }
 
@@ -438,10 +467,12 @@ int ce_nn_get_state(ce_nn_engine *e, float *theta, float *gprev, int32_t *step, 
     const size_t E = e->cfg.num_envs, P = e->P, Ps = e->Ps, N = e->cfg.n_rows;
     CE_HIP(hipStreamSynchronize(e->stream));
     if (theta)
-        CE_HIP(hipMemcpy2D(theta, P * sizeof(float), e->theta, Ps * sizeof(float), P * sizeof(float),
+        CE_HIP(hipMemcpy2D(theta, P * sizeof(float), e->theta_buf[e->parity], Ps * sizeof(float),
+                           P * sizeof(float),
                            E, hipMemcpyDeviceToHost));
     if (gprev)
-        CE_HIP(hipMemcpy2D(gprev, P * sizeof(float), e->gprev, Ps * sizeof(float), P * sizeof(float),
+        CE_HIP(hipMemcpy2D(gprev, P * sizeof(float), e->g_buf[e->parity], Ps * sizeof(float),
+                           P * sizeof(float),
                            E, hipMemcpyDeviceToHost));
     if (step) CE_HIP(hipMemcpy(step, e->step, E * sizeof(int32_t), hipMemcpyDeviceToHost));
     if (cursor) CE_HIP(hipMemcpy(cursor, e->cursor, E * sizeof(int32_t), hipMemcpyDeviceToHost));

@@ -1,24 +1,25 @@
 // MultiOptLRs-v0 over the OptimizeNN problem for gfx950.
 //
-// One OptVecEnv.step of E envs = two launches, one 512-thread workgroup per
-// env in each:
-//   nn_grad_kernel   MultiOptLRs.base_step up to the update
-//                    (custom_envs/envs/multioptlrs.py:81-87):
-//                      grad = model.get_gradient()   forward + backward of the
-//                        F -> hidden... (relu) -> K softmax network on the
-//                        current batch (problems/optimize_nn.py:35-52,122-126)
-//                      lr = 10^(a - 4)                (utils/utils_env.py:113-114)
-//                      theta' = theta - grad * lr     -> theta_n
-//                    and, for an env that was just reset, the reset's
-//                    model.get() (multioptlrs.py:70-71): same weights, same
-//                    batch, so the same gradient seeds the raw history.
-//   nn_step_kernel   the rest of base_step (multioptlrs.py:88-129):
-//                      grad, loss = model.get()       at theta' on the same batch
-//                      History append, observation v3 ratios, adjusted
-//                      history, obs = clip(nan_to_num(.), +-100) - 1,
-//                      reward v6, early stop, the 14 info values
-//                      model.next()                   (optimize_nn.py:102-112)
-//                    then OptVecEnv's auto-reset (concurrentvecenv.py:37).
+// One OptVecEnv.step of E envs is five launches on one stream:
+//   nn_grad_kernel      (one 512-thread workgroup per env) grad =
+//                       model.get_gradient(): forward + backward of the
+//                       F -> hidden... (relu) -> K softmax network on the
+//                       current batch (multioptlrs.py:85, optimize_nn.py:
+//                       35-52,122-126); for an env just reset this is also the
+//                       reset's model.get() (multioptlrs.py:70-71)
+//   nn_update_kernel    (four agents per thread) lr = 10^(a - 4)
+//                       (utils_env.py:113-114), theta' = theta - grad * lr
+//   nn_step_kernel      (per env) grad, loss = model.get() at theta'
+//                       (multioptlrs.py:88)
+//   nn_agent_kernel     (per agent) History append, observation v3 ratios,
+//                       adjusted history, obs = clip(nan_to_num(.), +-100) - 1
+//                       (multioptlrs.py:89-101, utils_env.py:155-161)
+//   nn_finalize_kernel  (per env) reward v6, early stop, the 14 info values
+//                       (multioptlrs.py:102-127), model.next() (optimize_nn.py:
+//                       102-112) and OptVecEnv's auto-reset (concurrentvecenv.py:37)
+// The per-env kernels are MFMA work with the whole network state of one env
+// in LDS; the per-agent kernels stream the HBM state with every load of an
+// agent issued before its stores, on a grid of env x (P / 256) blocks.
 //
 // Matrices run on v_mfma_f32_32x32x2_f32.  Every activation lives in LDS
 // sample-major ([32 samples][width + 4]); each GEMM picks the operand roles
@@ -32,9 +33,8 @@
 //   dW        (in units x out units) = H^T . dZ : reduction over the 32
 //             samples, s = 2c + h; element (i, j) of the C tile is flat
 //             parameter off + i * w_out + j, lanes contiguous along j.
-// The output layer (K <= 32 classes) is VALU work.  Each gradient element is
-// handed to the kernel's per-element epilogue straight from the accumulator
-// registers, so the gradient never makes an HBM round trip.
+// The output layer (K <= 32 classes) is VALU work.  Gradients leave the
+// accumulator registers as one coalesced store per element.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -63,6 +63,9 @@ constexpr int kNnMaxWidth = 512;   // hidden units per layer (multiple of 32)
 constexpr int kNnMaxK = 32;        // classes
 constexpr int kNnMaxH = 16;        // adjusted-history length
 constexpr int kNnPad = 4;          // LDS row padding (floats)
+constexpr int kNnChunk = 256;      // threads (and agents) per block of nn_agent_kernel
+constexpr int kNnUpdPer = 4;       // agents per thread of nn_update_kernel
+constexpr int kNnPrefetch = 8;     // 8-float k-chunks of W in flight per lane
 
 struct NnArgs {
     int E, N, F, K, L, B, nb, H, max_batches, auto_reset;
@@ -71,20 +74,29 @@ struct NnArgs {
     int dims[kNnMaxHidden + 2];    // F, hidden..., K
     int off_w[kNnMaxHidden + 1];   // flat offset of layer l's kernel [dims[l]][dims[l+1]]
     int off_b[kNnMaxHidden + 1];   // flat offset of layer l's bias
-    int lds_x, lds_h[kNnMaxHidden], lds_z, lds_part, lds_bytes;   // float offsets
+    int lds_x, lds_h[kNnMaxHidden], lds_z, lds_wo, lds_part, lds_bytes;   // float offsets
     int split;                     // 1: some hidden forward needs the split-k scratch
     const float *X;                // [N][F] dataset rows (dataset order)
     const int32_t *label;          // [N]
+    // theta/theta_n and gprev/gN are two ping-pong pairs: the engine swaps
+    // them every step, so theta' and the new gradient become current
+    // without a copy
     float *theta;                  // [E][Ps] current parameters
     float *theta_n;                // [E][Ps] parameters after this step's update
     const float *theta0;           // [E][Ps] reset parameters
     float *gprev;                  // [E][Ps] newest raw-history gradient
+    float *gN;                     // [E][Ps] gradient at theta' (this step's entry)
+    float *gU;                     // [E][Ps] gradient at theta (the update's)
+    float *loss_b;                 // [E] minibatch loss at theta'
+    double *part_u;                // [E][nchunk_u][3] update sums (lr, lr^2, reset gradient)
+    double *part_c;                // [E][nchunk][5] agent sums (|theta'|, |w~|, |g~|, g, |dg|)
+    int nchunk;                    // nn_agent_kernel blocks per env (kNnChunk agents each)
+    int nchunk_u;                  // nn_update_kernel blocks per env
     float *rw, *rg;                // [H][E][Ps] adjusted w~ / g~ entries, obs form
     double *al;                    // [H][E] adjusted loss entries (raw)
     double *sw, *sg;               // [H][E] sum |w~|, sum |g~| of each entry
     float *hl;                     // [5][E] raw-history losses
     double *hsg;                   // [5][E] raw-history gradient sums
-    double *lr_stats;              // [E][2] sum lr, sum lr^2 of this step
     int32_t *step;                 // [E]
     int32_t *cursor;               // [E] current batch index within the epoch
     int32_t *order;                // [2][E][N] row order (ping-pong)
@@ -142,23 +154,30 @@ __device__ void nn_forward_hidden(const float *W, const float *bias, int w_in, i
         const int j = tile * 32 + li;
         nn_f32x16 acc = {};
         const float *xrow = in + li * ld_in + 4 * h;
-        float wn[4];
-        float4 xn = {};
-        auto load = [&](int c) {
-            xn = *reinterpret_cast<const float4 *>(xrow + 8 * c);
+        // W fragments stream from HBM kNnPrefetch chunks ahead (a register
+        // ring refilled right after use); the X rows come from LDS at use
+        float wb[kNnPrefetch][4];
+        auto loadw = [&](int c, float (&w)[4]) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const int k = 8 * c + 4 * h + m;
-                wn[m] = k < w_in ? W[static_cast<size_t>(k) * w_out + j] : 0.0f;
+                w[m] = (c < c1 && k < w_in) ? W[static_cast<size_t>(k) * w_out + j] : 0.0f;
             }
         };
-        if (c0 < c1) load(c0);
-        for (int c = c0; c < c1; ++c) {
-            const float xs[4] = {xn.x, xn.y, xn.z, xn.w};
-            const float wc[4] = {wn[0], wn[1], wn[2], wn[3]};
-            if (c + 1 < c1) load(c + 1);
 #pragma unroll
-            for (int m = 0; m < 4; ++m) acc = nn_mfma(wc[m], xs[m], acc);
+        for (int d = 0; d < kNnPrefetch; ++d) loadw(c0 + d, wb[d]);
+        for (int c = c0; c < c1; c += kNnPrefetch) {
+#pragma unroll
+            for (int d = 0; d < kNnPrefetch; ++d) {
+                if (c + d < c1) {
+                    const float4 x = *reinterpret_cast<const float4 *>(xrow + 8 * (c + d));
+                    acc = nn_mfma(wb[d][0], x.x, acc);
+                    acc = nn_mfma(wb[d][1], x.y, acc);
+                    acc = nn_mfma(wb[d][2], x.z, acc);
+                    acc = nn_mfma(wb[d][3], x.w, acc);
+                }
+                loadw(c + kNnPrefetch + d, wb[d]);
+            }
         }
         // lane holds sample li, units tile*32 + nn_acc_row(r, h): r = 4g..4g+3
         // are 4 consecutive units
@@ -296,7 +315,7 @@ __device__ __forceinline__ void nn_backward(const NnArgs &a, const float *theta,
         if (L == 0) return;
         // dH_L[s][j] = sum_k dZ[s][k] W_out[j][k], masked by H_L > 0: 32 x w
         // values, w / 16 per thread, written back after every read of H_L
-        const float *Wo = theta + ow;
+        const float *Wo = lds + a.lds_wo;          // staged by nn_forward
         constexpr int kPer = kNnMaxWidth * kNnBatch / kNnBlock;
         float dh[kPer];
         const int per = w * kNnBatch / kNnBlock;
@@ -352,13 +371,26 @@ __device__ __forceinline__ void nn_backward(const NnArgs &a, const float *theta,
                 if (tile < tin) {
                     const float *wrow = W + static_cast<size_t>(tile * 32 + li) * w_out + 4 * h;
                     const float *zrow = dz + li * ldo + 4 * h;
-                    for (int c = 0; c < chunks; ++c) {
-                        const float4 wa = *reinterpret_cast<const float4 *>(wrow + 8 * c);
-                        const float4 zv = *reinterpret_cast<const float4 *>(zrow + 8 * c);
-                        acc = nn_mfma(wa.x, zv.x, acc);
-                        acc = nn_mfma(wa.y, zv.y, acc);
-                        acc = nn_mfma(wa.z, zv.z, acc);
-                        acc = nn_mfma(wa.w, zv.w, acc);
+                    float4 wb[kNnPrefetch];
+#pragma unroll
+                    for (int d = 0; d < kNnPrefetch; ++d)
+                        wb[d] = d < chunks ? *reinterpret_cast<const float4 *>(wrow + 8 * d)
+                                           : float4{0.0f, 0.0f, 0.0f, 0.0f};
+                    for (int c = 0; c < chunks; c += kNnPrefetch) {
+#pragma unroll
+                        for (int d = 0; d < kNnPrefetch; ++d) {
+                            if (c + d < chunks) {
+                                const float4 zv =
+                                    *reinterpret_cast<const float4 *>(zrow + 8 * (c + d));
+                                acc = nn_mfma(wb[d].x, zv.x, acc);
+                                acc = nn_mfma(wb[d].y, zv.y, acc);
+                                acc = nn_mfma(wb[d].z, zv.z, acc);
+                                acc = nn_mfma(wb[d].w, zv.w, acc);
+                            }
+                            const int cn = c + kNnPrefetch + d;
+                            if (cn < chunks)
+                                wb[d] = *reinterpret_cast<const float4 *>(wrow + 8 * cn);
+                        }
                     }
                 }
                 dht[q] = acc;
@@ -414,6 +446,10 @@ __device__ __forceinline__ void nn_backward(const NnArgs &a, const float *theta,
 __device__ float nn_forward(const NnArgs &a, const float *theta, float *lds, const int *rows,
                             int nrows, float *red) {
     const int L = a.L;
+    // the output layer's kernel [dims[L]][K] (a few KB) is read by every
+    // thread of the logits and dH_L passes: stage it once
+    for (int i = threadIdx.x; i < a.dims[L] * a.K; i += kNnBlock)
+        lds[a.lds_wo + i] = theta[a.off_w[L] + i];
     for (int l = 0; l < L; ++l) {
         const float *in = lds + (l ? a.lds_h[l - 1] : a.lds_x);
         nn_forward_hidden(theta + a.off_w[l], theta + a.off_b[l], a.dims[l], a.dims[l + 1], in,
@@ -422,15 +458,16 @@ __device__ float nn_forward(const NnArgs &a, const float *theta, float *lds, con
         __syncthreads();
     }
     const float *hl = lds + (L ? a.lds_h[L - 1] : a.lds_x);
-    nn_forward_logits(theta + a.off_w[L], theta + a.off_b[L], a.dims[L], a.K, hl,
+    nn_forward_logits(lds + a.lds_wo, theta + a.off_b[L], a.dims[L], a.K, hl,
                       nn_ld(a.dims[L]), lds + a.lds_z, nn_ld(a.K));
     __syncthreads();
     return nn_softmax_ce(a, rows, nrows, lds + a.lds_z, nn_ld(a.K), red);
 }
 
 // block-wide float64 sums of NV values per thread (wave butterfly + LDS)
-template <int NV>
+template <int NV, int BLOCK>
 __device__ __forceinline__ void nn_block_sum(double (&v)[NV], double *red) {
+    constexpr int kW = BLOCK / 64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < NV; ++k)
@@ -442,7 +479,7 @@ __device__ __forceinline__ void nn_block_sum(double (&v)[NV], double *red) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         double s = 0.0;
-        for (int w = 0; w < kNnWaves; ++w) s += red[w * NV + k];
+        for (int w = 0; w < kW; ++w) s += red[w * NV + k];
         v[k] = s;
     }
     __syncthreads();
@@ -452,191 +489,277 @@ __device__ __forceinline__ float nn_lr(float act) {
     return static_cast<float>(exp10(static_cast<double>(act - 4.0f)));
 }
 
-// ------------------------------------------------------------------ kernels
-struct NnGradEmit {
-    const float *theta, *act;
-    float *theta_n, *gprev;
-    const int32_t *agent_row;
-    bool fresh;
-    double lr_sum = 0.0, lr_sq = 0.0, g_sum = 0.0;
-    __device__ __forceinline__ void operator()(int p, float g) {
-        const float lr = nn_lr(act[agent_row[p]]);
-        theta_n[p] = theta[p] - g * lr;
-        lr_sum += lr;
-        lr_sq += static_cast<double>(lr) * lr;
-        if (fresh) {
-            gprev[p] = g;
-            g_sum += g;
-        }
-    }
+// ------------------------------------------------------------- eval kernels
+// The gradient of one forward+backward goes to an [E][Ps] buffer with one
+// coalesced store per element (32 lanes x 4 B per accumulator register).
+struct NnStore {
+    float *g;
+    __device__ __forceinline__ void operator()(int p, float v) const { g[p] = v; }
 };
 
-__global__ __launch_bounds__(kNnBlock, 2) void nn_grad_kernel(NnArgs a) {
-#pragma clang fp contract(off)
-    extern __shared__ float lds[];
-    __shared__ int rows[kNnBatch];
-    __shared__ double red[kNnWaves * 4];
-    const size_t e = blockIdx.x;
-    const size_t ps = a.Ps;
+__device__ __forceinline__ float nn_eval(const NnArgs &a, size_t e, const float *theta, float *g,
+                                         float *lds, int *rows, float *red) {
     const int nrows = nn_stage_batch(a, e, lds, rows);
     __syncthreads();
-    const float *theta = a.theta + e * ps;
-    const float loss = nn_forward(a, theta, lds, rows, nrows, reinterpret_cast<float *>(red));
+    const float loss = nn_forward(a, theta, lds, rows, nrows, red);
+    NnStore st{g};
+    nn_backward(a, theta, lds, st);
+    return loss;
+}
+
+// model.get_gradient() at theta (multioptlrs.py:85); for an env that was
+// just reset it is also the reset's model.get() (multioptlrs.py:70-71):
+// same weights, same batch, so it seeds the raw history [l0, 0, 0, 0, 0].
+__global__ __launch_bounds__(kNnBlock, 4) void nn_grad_kernel(NnArgs a) {
+    extern __shared__ float lds[];
+    __shared__ int rows[kNnBatch];
+    __shared__ float red[4];
+    const size_t e = blockIdx.x, ps = a.Ps;
+    const float loss = nn_eval(a, e, a.theta + e * ps, a.gU + e * ps, lds, rows, red);
+    if (threadIdx.x == 0 && a.step[e] == 0)
+        for (int k = 0; k < kRawHist; ++k) a.hl[k * a.E + e] = k == 0 ? loss : 0.0f;
+}
+
+// model.get() at theta' on the same batch (multioptlrs.py:88)
+__global__ __launch_bounds__(kNnBlock, 4) void nn_step_kernel(NnArgs a) {
+    extern __shared__ float lds[];
+    __shared__ int rows[kNnBatch];
+    __shared__ float red[4];
+    const size_t e = blockIdx.x, ps = a.Ps;
+    const float loss = nn_eval(a, e, a.theta_n + e * ps, a.gN + e * ps, lds, rows, red);
+    if (threadIdx.x == 0) a.loss_b[e] = loss;
+}
+
+// ------------------------------------------------------- elementwise kernels
+// One thread per (env, agent); blocks of kNnChunk consecutive agents of one
+// env (blockIdx.x = chunk, blockIdx.y = env), every load issued before any
+// store so a wave keeps all its memory traffic in flight at once.
+
+// the update (multioptlrs.py:86-87): lr = 10^(a - 4), theta' = theta - g lr;
+// per-chunk sums of lr, lr^2 (actions_mean/std) and, after a reset, of the
+// reset gradient (the raw history's first entry).  kNnUpdPer agents per
+// thread, strided by the block so every load stays coalesced: the action
+// gather (through the sorted-name row table) is the second round trip, and
+// four agents' worth of it is in flight at once.
+__global__ __launch_bounds__(kNnChunk) void nn_update_kernel(NnArgs a) {
+#pragma clang fp contract(off)
+    __shared__ double red[(kNnChunk / 64) * 3];
+    const size_t e = blockIdx.y, ps = a.Ps;
+    const int chunk = blockIdx.x;
+    const int base = chunk * kNnChunk * kNnUpdPer + threadIdx.x;
     const bool fresh = a.step[e] == 0;
-    NnGradEmit em{theta, a.act + e * a.P, a.theta_n + e * ps, a.gprev + e * ps, a.agent_row,
-                  fresh};
-    nn_backward(a, theta, lds, em);
-    double v[3] = {em.lr_sum, em.lr_sq, em.g_sum};
-    nn_block_sum<3>(v, red);
-    if (threadIdx.x == 0) {
-        a.lr_stats[2 * e] = v[0];
-        a.lr_stats[2 * e + 1] = v[1];
-        if (fresh) {
-            // the reset's History: [entry of model.get() at theta0, 0, 0, 0, 0]
-            for (int k = 0; k < kRawHist; ++k) {
-                a.hl[k * a.E + e] = k == 0 ? loss : 0.0f;
-                a.hsg[k * a.E + e] = k == 0 ? v[2] : 0.0;
+    const float *act = a.act + e * a.P;
+    const float *gu = a.gU + e * ps, *th = a.theta + e * ps;
+    float g[kNnUpdPer], t[kNnUpdPer], av[kNnUpdPer];
+    int row[kNnUpdPer];
+#pragma unroll
+    for (int q = 0; q < kNnUpdPer; ++q) {
+        const int p = base + q * kNnChunk;
+        const int pc = p < a.P ? p : 0;
+        g[q] = gu[pc];
+        t[q] = th[pc];
+        row[q] = a.agent_row[pc];
+    }
+#pragma unroll
+    for (int q = 0; q < kNnUpdPer; ++q) av[q] = act[row[q]];
+    double v[3] = {0.0, 0.0, 0.0};
+    float *tn = a.theta_n + e * ps, *gp = a.gprev + e * ps;
+#pragma unroll
+    for (int q = 0; q < kNnUpdPer; ++q) {
+        const int p = base + q * kNnChunk;
+        if (p < a.P) {
+            const float lr = nn_lr(av[q]);
+            tn[p] = t[q] - g[q] * lr;
+            v[0] += lr;
+            v[1] += static_cast<double>(lr) * lr;
+            if (fresh) {
+                gp[p] = g[q];
+                v[2] += g[q];
             }
         }
+    }
+    nn_block_sum<3, kNnChunk>(v, red);
+    if (threadIdx.x == 0) {
+        double *o = a.part_u + (e * a.nchunk_u + chunk) * 3;
+        o[0] = v[0];
+        o[1] = v[1];
+        o[2] = v[2];
     }
 }
 
-struct NnStepEmit {
-    // copies of the argument fields used per element (a pointer to the
-    // kernel argument block would force it into scratch)
-    float *theta, *gprev, *rw, *rg, *obs;
-    const float *theta_n, *theta0;
-    const int32_t *agent_row;
-    size_t plane;                  // E * Ps: stride between ring slots
-    size_t obs_base;               // e * P
-    int s, H, slot;                // step, history length, adjusted slot of this step
-    bool wipe;
-    const float *lobs;             // [H] l~ entries in obs form, age order (LDS)
-    double sum_w = 0.0, sum_aw = 0.0, sum_ag = 0.0, sum_g = 0.0, sum_gd = 0.0;
-    __device__ __forceinline__ void operator()(int p, float g) {
-        const float th_old = theta[p];
-        const float th_new = theta_n[p];
-        const float gp = gprev[p];
-        const double adj_w = ratio(th_new, th_old);
-        const double adj_g = ratio(g, gp);
-        sum_w += fabs(static_cast<double>(th_new));
-        sum_aw += fabs(adj_w);
-        sum_ag += fabs(adj_g);
-        sum_g += g;
-        sum_gd += fabs(static_cast<double>(g) - static_cast<double>(gp));
-        const float ow = static_cast<float>(clip100(adj_w) - 1.0);
-        const float og = static_cast<float>(clip100(adj_g) - 1.0);
-        float *dst = obs + (obs_base + agent_row[p]) * (3 * static_cast<size_t>(H));
-        for (int k = 0; k < H; ++k) {
-            float wk, gk, lk;
-            if (wipe) {
-                wk = gk = lk = -1.0f;
-            } else if (k == 0) {
-                wk = ow;
-                gk = og;
-                lk = lobs[0];
-            } else if (k < s) {
-                const int sl = ((slot - k) % H + H) % H;
-                wk = rw[sl * plane + p];
-                gk = rg[sl * plane + p];
-                lk = lobs[k];
-            } else {
-                wk = gk = lk = -1.0f;          // clip(0) - 1: the reset zeros
-            }
-            dst[k] = wk;
-            dst[H + k] = lk;
-            dst[2 * H + k] = gk;
-        }
-        rw[slot * plane + p] = ow;
-        rg[slot * plane + p] = og;
-        gprev[p] = g;
-        theta[p] = wipe ? theta0[p] : th_new;
-    }
+// per-env scalars every agent of a step shares (multioptlrs.py:88-107)
+struct NnStepScalars {
+    int s, slot, slot5;
+    float loss;
+    double adj_l, reward;
+    bool terminal, wipe;
 };
 
-__global__ __launch_bounds__(kNnBlock, 2) void nn_step_kernel(NnArgs a) {
-#pragma clang fp contract(off)
-    extern __shared__ float lds[];
-    __shared__ int rows[kNnBatch];
-    __shared__ double red[kNnWaves * 5];
-    __shared__ int32_t comp[1];
-    __shared__ float lobs[kNnMaxH];
-    const size_t e = blockIdx.x;
-    const size_t ps = a.Ps, E = a.E;
-    const int tid = threadIdx.x, H = a.H;
-    const int nrows = nn_stage_batch(a, e, lds, rows);
-    __syncthreads();
-    const float *theta_n = a.theta_n + e * ps;
-    const float loss = nn_forward(a, theta_n, lds, rows, nrows, reinterpret_cast<float *>(red));
-
-    // History append (raw, 5 entries) and observation v3 of the loss
-    const int s = a.step[e] + 1;
-    const int slot5 = s % kRawHist, prev5 = (s - 1) % kRawHist;
-    const float l_prev = a.hl[prev5 * E + e];
-    const double adj_l = ratio(loss, l_prev);
-    const int slot = (s - 1) % H;
-    double reward = 1.0 - adj_l;
+__device__ __forceinline__ NnStepScalars nn_step_scalars(const NnArgs &a, size_t e) {
+    NnStepScalars r;
+    const size_t E = a.E;
+    r.s = a.step[e] + 1;
+    r.slot = (r.s - 1) % a.H;
+    r.slot5 = r.s % kRawHist;
+    r.loss = a.loss_b[e];
+    const float l_prev = a.hl[((r.s - 1) % kRawHist) * E + e];
+    r.adj_l = ratio(r.loss, l_prev);
+    double reward = 1.0 - r.adj_l;
     reward = reward < -100.0 ? -100.0 : (reward > 100.0 ? 100.0 : reward);
-    bool terminal = s >= a.max_batches;
-    if (!terminal && loss > 1e4f) {
-        terminal = true;
-        reward -= static_cast<double>(a.max_batches - s);
+    r.terminal = r.s >= a.max_batches;
+    if (!r.terminal && r.loss > 1e4f) {
+        r.terminal = true;
+        reward -= static_cast<double>(a.max_batches - r.s);
     }
-    const bool wipe = terminal && a.auto_reset;
+    r.reward = reward;
+    r.wipe = r.terminal && a.auto_reset;
+    return r;
+}
 
-    NnStepEmit em;
-    em.theta = a.theta + e * ps;
-    em.gprev = a.gprev + e * ps;
-    em.rw = a.rw + e * ps;
-    em.rg = a.rg + e * ps;
-    em.obs = a.obs;
-    em.theta_n = theta_n;
-    em.theta0 = a.theta0 + e * ps;
-    em.agent_row = a.agent_row;
-    em.plane = E * ps;
-    em.obs_base = e * a.P;
-    em.s = s;
-    em.H = H;
-    em.slot = slot;
-    em.wipe = wipe;
+// History append + observation v3 + adjusted history + obs rows
+// (multioptlrs.py:89-101), then theta <- theta' (or theta0 on auto-reset)
+__global__ __launch_bounds__(kNnChunk) void nn_agent_kernel(NnArgs a) {
+#pragma clang fp contract(off)
+    extern __shared__ float stage[];               // [kNnChunk][3H] obs rows
+    __shared__ int rows_s[kNnChunk];
+    __shared__ float lobs[kNnMaxH];
+    __shared__ double red[(kNnChunk / 64) * 5];
+    const size_t e = blockIdx.y, ps = a.Ps, E = a.E;
+    const int chunk = blockIdx.x, tid = threadIdx.x, H = a.H;
+    const int p0 = chunk * kNnChunk;
+    const int p = p0 + tid;
+    const bool on = p < a.P;
+    const int pc = on ? p : 0;
+    const NnStepScalars sc = nn_step_scalars(a, e);
+    const int s = sc.s, slot = sc.slot;
+    const size_t ep = e * ps + pc, plane = E * ps;
+
+    // ---- every load of the agent up front
+    const float th_old = a.theta[ep];
+    const float th_new = a.theta_n[ep];
+    const float gp = a.gprev[ep];
+    const float g = a.gN[ep];
+    const int row = a.agent_row[pc];
+    float rwv[kNnMaxH], rgv[kNnMaxH];
+#pragma unroll
+    for (int k = 1; k < kNnMaxH; ++k) {
+        if (k < H && k < s) {                       // block-uniform
+            const int sl = ((slot - k) % H + H) % H;
+            rwv[k] = a.rw[sl * plane + ep];
+            rgv[k] = a.rg[sl * plane + ep];
+        } else {
+            rwv[k] = rgv[k] = -1.0f;                // clip(0) - 1: the reset zeros
+        }
+    }
     if (tid < H) {
         const int k = tid;
         double lk = 0.0;
-        if (k == 0) lk = adj_l;
+        if (k == 0) lk = sc.adj_l;
         else if (k < s) lk = a.al[(((slot - k) % H + H) % H) * E + e];
         lobs[k] = static_cast<float>(clip100(lk) - 1.0);
     }
-    em.lobs = lobs;
-    __syncthreads();
-    nn_backward(a, theta_n, lds, em);
-    double v[5] = {em.sum_w, em.sum_aw, em.sum_ag, em.sum_g, em.sum_gd};
-    nn_block_sum<5>(v, red);
+    rows_s[tid] = on ? row : -1;
 
-    const int P = a.P;
+    const double adj_w = ratio(th_new, th_old);
+    const double adj_g = ratio(g, gp);
+    const float ow = static_cast<float>(clip100(adj_w) - 1.0);
+    const float og = static_cast<float>(clip100(adj_g) - 1.0);
+    double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    if (on) {
+        v[0] = fabs(static_cast<double>(th_new));
+        v[1] = fabs(adj_w);
+        v[2] = fabs(adj_g);
+        v[3] = g;
+        v[4] = fabs(static_cast<double>(g) - static_cast<double>(gp));
+        a.rw[slot * plane + ep] = ow;
+        a.rg[slot * plane + ep] = og;
+        if (sc.wipe) a.theta_n[ep] = a.theta0[ep];   // theta_n is current next step
+    }
+    __syncthreads();
+    // ---- the agent's row [w~ (H, newest first) | l~ (H) | g~ (H)] in LDS
+    const int W = 3 * H;
+    float *st = stage + tid * W;
+#pragma unroll
+    for (int k = 0; k < kNnMaxH; ++k) {
+        if (k < H) {
+            const bool reset_row = sc.wipe;
+            st[k] = reset_row ? -1.0f : (k == 0 ? ow : rwv[k]);
+            st[H + k] = reset_row ? -1.0f : lobs[k];
+            st[2 * H + k] = reset_row ? -1.0f : (k == 0 ? og : rgv[k]);
+        }
+    }
+    __syncthreads();
+    // ---- rows out: flat (agent j, entry k) across the block, so a wave's
+    // stores cover whole runs of consecutive rows (consecutive agents are
+    // consecutive rows in sorted-name order within each decade)
+    const int n = (a.P - p0 < kNnChunk ? a.P - p0 : kNnChunk) * W;
+    float *obs = a.obs + e * static_cast<size_t>(a.P) * W;
+    const int dj = kNnChunk / W, dk = kNnChunk - dj * W;   // uniform step of (j, k)
+    int j = tid / W, k = tid - (tid / W) * W;
+    for (int f = tid; f < n; f += kNnChunk) {
+        obs[static_cast<size_t>(rows_s[j]) * W + k] = stage[f];
+        j += dj;
+        k += dk;
+        if (k >= W) {
+            k -= W;
+            ++j;
+        }
+    }
+    nn_block_sum<5, kNnChunk>(v, red);
     if (tid == 0) {
-        // rings: this step's entries, then the info sums over them
-        a.al[slot * E + e] = adj_l;
-        a.sw[slot * E + e] = v[1];
-        a.sg[slot * E + e] = v[2];
-        a.hl[slot5 * E + e] = loss;
-        a.hsg[slot5 * E + e] = v[3];
+        double *o = a.part_c + (e * a.nchunk + chunk) * 5;
+        for (int k = 0; k < 5; ++k) o[k] = v[k];
+    }
+}
+
+// reward, info, rings of per-step sums, step counter, model.next() and the
+// auto-reset's row order (multioptlrs.py:102-128, optimize_nn.py:102-120)
+__global__ __launch_bounds__(kNnChunk) void nn_finalize_kernel(NnArgs a) {
+    __shared__ double red[(kNnChunk / 64) * 8];
+    __shared__ int32_t comp[1];
+    const size_t e = blockIdx.x, E = a.E;
+    const int tid = threadIdx.x, H = a.H, P = a.P;
+    double v[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int c = tid; c < a.nchunk_u; c += kNnChunk) {
+        const double *u = a.part_u + (e * a.nchunk_u + c) * 3;
+        v[0] += u[0];
+        v[1] += u[1];
+        v[2] += u[2];
+    }
+    for (int c = tid; c < a.nchunk; c += kNnChunk) {
+        const double *q = a.part_c + (e * a.nchunk + c) * 5;
+        for (int k = 0; k < 5; ++k) v[3 + k] += q[k];
+    }
+    nn_block_sum<8, kNnChunk>(v, red);
+    const NnStepScalars sc = nn_step_scalars(a, e);
+    const int s = sc.s;
+    if (tid == 0) {
+        if (s == 1) {
+            // the reset's raw-history gradient entry (nn_update_kernel sums)
+            for (int k = 0; k < kRawHist; ++k) a.hsg[k * E + e] = k == 0 ? v[2] : 0.0;
+        }
+        a.al[sc.slot * E + e] = sc.adj_l;
+        a.sw[sc.slot * E + e] = v[4];
+        a.sg[sc.slot * E + e] = v[5];
+        a.hl[sc.slot5 * E + e] = sc.loss;
+        a.hsg[sc.slot5 * E + e] = v[6];
         double lsum = 0.0, gsum = 0.0, st = 0.0;
         for (int k = 0; k < kRawHist; ++k) {
             lsum += a.hl[k * E + e];
             gsum += a.hsg[k * E + e];
         }
         for (int k = 0; k < H && k < s; ++k) {
-            const int sl = ((slot - k) % H + H) % H;
+            const int sl = ((sc.slot - k) % H + H) % H;
             st += a.sw[sl * E + e] + a.sg[sl * E + e] + P * fabs(a.al[sl * E + e]);
         }
         const double n = P;
-        const double amean = a.lr_stats[2 * e] / n;
-        const double avar = fmax(a.lr_stats[2 * e + 1] / n - amean * amean, 0.0);
+        const double amean = v[0] / n;
+        const double avar = fmax(v[1] / n - amean * amean, 0.0);
         float *info = a.info + e * kMultiInfo;
-        info[0] = terminal ? loss : __builtin_nanf("");
-        info[1] = loss;
-        info[2] = static_cast<float>(v[0] / n);
-        info[3] = static_cast<float>(v[0]);
+        info[0] = sc.terminal ? sc.loss : __builtin_nanf("");
+        info[1] = sc.loss;
+        info[2] = static_cast<float>(v[3] / n);
+        info[3] = static_cast<float>(v[3]);
         info[4] = static_cast<float>(amean);
         info[5] = static_cast<float>(sqrt(avar));
         info[6] = static_cast<float>(st / (n * 3 * H));
@@ -644,23 +767,21 @@ __global__ __launch_bounds__(kNnBlock, 2) void nn_step_kernel(NnArgs a) {
         info[8] = static_cast<float>(gsum / (kRawHist * n));
         info[9] = static_cast<float>(gsum);
         info[10] = static_cast<float>(lsum / kRawHist);
-        info[11] = static_cast<float>(adj_l);
-        info[12] = static_cast<float>(v[2] / n);
-        info[13] = static_cast<float>(v[4] / n);
+        info[11] = static_cast<float>(sc.adj_l);
+        info[12] = static_cast<float>(v[5] / n);
+        info[13] = static_cast<float>(v[7] / n);
         a.episode_len[e] = s;
-        a.step[e] = wipe ? 0 : s;
-        // model.next() (optimize_nn.py:102-112), then the reset's
-        // on_epoch_end when the env restarts; both compose the row order
+        a.step[e] = sc.wipe ? 0 : s;
         const int cur = a.cursor[e] + 1;
         const bool wrap = cur >= a.nb;
-        a.cursor[e] = wipe || wrap ? 0 : cur;
-        comp[0] = (wrap ? 1 : 0) | (wipe ? 2 : 0);
+        a.cursor[e] = sc.wipe || wrap ? 0 : cur;
+        comp[0] = (wrap ? 1 : 0) | (sc.wipe ? 2 : 0);
     }
     // reward / done rows (replicated per agent, optvecenv.py:43-45)
-    const float rw = static_cast<float>(reward);
-    for (int r = tid; r < P; r += kNnBlock) {
+    const float rw = static_cast<float>(sc.reward);
+    for (int r = tid; r < P; r += kNnChunk) {
         a.reward[e * P + r] = rw;
-        a.done[e * P + r] = terminal ? 1 : 0;
+        a.done[e * P + r] = sc.terminal ? 1 : 0;
     }
     __syncthreads();
     const int c = comp[0];
@@ -669,7 +790,7 @@ __global__ __launch_bounds__(kNnBlock, 2) void nn_step_kernel(NnArgs a) {
         const int32_t *cur = a.order + (static_cast<size_t>(sel) * E + e) * a.N;
         int32_t *nxt = a.order + (static_cast<size_t>(1 - sel) * E + e) * a.N;
         const int32_t *pi = a.epoch_perm + e * a.N, *rho = a.reset_perm + e * a.N;
-        for (int i = tid; i < a.N; i += kNnBlock) {
+        for (int i = tid; i < a.N; i += kNnChunk) {
             int j = (c & 2) ? rho[i] : i;
             if (c & 1) j = pi[j];
             nxt[i] = cur[j];
