@@ -197,7 +197,8 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     e->P = a.P = static_cast<int>(P);
     e->Ps = static_cast<size_t>((P + 63) & ~63L);
     a.Ps = static_cast<int>(e->Ps);
-    a.nchunk = static_cast<int>((P + ce::kNnChunk - 1) / ce::kNnChunk);
+    a.nchunk = static_cast<int>((P + ce::kNnChunk * ce::kNnAgentPer - 1) /
+                                (ce::kNnChunk * ce::kNnAgentPer));
     a.nchunk_u = static_cast<int>((P + ce::kNnChunk * ce::kNnUpdPer - 1) /
                                   (ce::kNnChunk * ce::kNnUpdPer));
     // LDS: X, every hidden activation, the logits, the split-k scratch

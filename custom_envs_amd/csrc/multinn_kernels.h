@@ -65,6 +65,11 @@ constexpr int kNnMaxH = 16;        // adjusted-history length
 constexpr int kNnPad = 4;          // LDS row padding (floats)
 constexpr int kNnChunk = 256;      // threads (and agents) per block of nn_agent_kernel
 constexpr int kNnUpdPer = 4;       // agents per thread of nn_update_kernel
+#ifndef CE_NN_AGENT_PER
+#define CE_NN_AGENT_PER 1
+#endif
+constexpr int kNnAgentPer = CE_NN_AGENT_PER;   // agents per thread of nn_agent_kernel
+constexpr int kNnRegH = 8;         // ring ages nn_agent_kernel holds in registers
 constexpr int kNnPrefetch = 8;     // 8-float k-chunks of W in flight per lane
 
 struct NnArgs {
@@ -90,7 +95,7 @@ struct NnArgs {
     float *loss_b;                 // [E] minibatch loss at theta'
     double *part_u;                // [E][nchunk_u][3] update sums (lr, lr^2, reset gradient)
     double *part_c;                // [E][nchunk][5] agent sums (|theta'|, |w~|, |g~|, g, |dg|)
-    int nchunk;                    // nn_agent_kernel blocks per env (kNnChunk agents each)
+    int nchunk;                    // nn_agent_kernel blocks per env (kNnChunk * kNnAgentPer agents)
     int nchunk_u;                  // nn_update_kernel blocks per env
     float *rw, *rg;                // [H][E][Ps] adjusted w~ / g~ entries, obs form
     double *al;                    // [H][E] adjusted loss entries (raw)
@@ -113,6 +118,22 @@ struct NnArgs {
 };
 
 __device__ __forceinline__ int nn_ld(int w) { return ((w + 31) & ~31) + kNnPad; }
+
+// numpy.nan_to_num(a / |b|) in float64 for float32 a, b (utils_env.py:155-161).
+// Finite operands with b != 0 take the hardware reciprocal, one Newton step
+// and one residual correction (the IEEE quotient up to a final-rounding tie,
+// far below the float32 the result is stored as); anything else takes the
+// IEEE division of ratio().  About a third of the float64 work of the
+// division sequence.
+__device__ __forceinline__ double nn_ratio(float a, float b) {
+    const double ad = a, bd = fabs(static_cast<double>(b));
+    if (!(bd > 0.0 && bd <= 3.4028234663852886e38 && fabs(ad) <= 3.4028234663852886e38))
+        return ratio(a, b);
+    double r = __builtin_amdgcn_rcp(bd);
+    r = fma(r, fma(-bd, r, 1.0), r);
+    const double q = ad * r;
+    return fma(fma(-bd, q, ad), r, q);
+}
 
 // ---------------------------------------------------------------- LDS staging
 // Batch rows of env e: order[sel][e][cursor * B + s], s < nrows; X rows
@@ -617,7 +638,14 @@ __device__ __forceinline__ NnStepScalars nn_step_scalars(const NnArgs &a, size_t
 }
 
 // History append + observation v3 + adjusted history + obs rows
-// (multioptlrs.py:89-101), then theta <- theta' (or theta0 on auto-reset)
+// (multioptlrs.py:89-101); on auto-reset theta_n (current next step) <- theta0.
+// kNnAgentPer agents per thread (strided by the block), every agent load
+// issued before the first use.  One agent per thread measured fastest (1.77
+// ms at 1024 envs against 1.82 for two and 2.08 for four: more agents per
+// thread cost occupancy and add staging barriers).  Obs rows go out through an LDS stage, one sub-chunk
+// of kNnChunk agents at a time, as flat (agent, entry) runs so a wave's
+// stores cover consecutive rows (sorted names keep each decade of agents in
+// consecutive rows).
 __global__ __launch_bounds__(kNnChunk) void nn_agent_kernel(NnArgs a) {
 #pragma clang fp contract(off)
     extern __shared__ float stage[];               // [kNnChunk][3H] obs rows
@@ -625,30 +653,37 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_kernel(NnArgs a) {
     __shared__ float lobs[kNnMaxH];
     __shared__ double red[(kNnChunk / 64) * 5];
     const size_t e = blockIdx.y, ps = a.Ps, E = a.E;
-    const int chunk = blockIdx.x, tid = threadIdx.x, H = a.H;
-    const int p0 = chunk * kNnChunk;
-    const int p = p0 + tid;
-    const bool on = p < a.P;
-    const int pc = on ? p : 0;
+    const int chunk = blockIdx.x, tid = threadIdx.x, H = a.H, W = 3 * H;
+    const int base = chunk * kNnChunk * kNnAgentPer;
     const NnStepScalars sc = nn_step_scalars(a, e);
     const int s = sc.s, slot = sc.slot;
-    const size_t ep = e * ps + pc, plane = E * ps;
+    const size_t plane = E * ps;
+    const float *th_old = a.theta + e * ps, *th_new = a.theta_n + e * ps;
+    const float *gpv = a.gprev + e * ps, *gnv = a.gN + e * ps;
+    const float *rw = a.rw + e * ps, *rg = a.rg + e * ps;
 
-    // ---- every load of the agent up front
-    const float th_old = a.theta[ep];
-    const float th_new = a.theta_n[ep];
-    const float gp = a.gprev[ep];
-    const float g = a.gN[ep];
-    const int row = a.agent_row[pc];
-    float rwv[kNnMaxH], rgv[kNnMaxH];
+    // ---- every load of the block's agents up front
+    float to[kNnAgentPer], tn[kNnAgentPer], gp[kNnAgentPer], g[kNnAgentPer];
+    float rwv[kNnAgentPer][kNnRegH], rgv[kNnAgentPer][kNnRegH];
+    int row[kNnAgentPer];
 #pragma unroll
-    for (int k = 1; k < kNnMaxH; ++k) {
-        if (k < H && k < s) {                       // block-uniform
-            const int sl = ((slot - k) % H + H) % H;
-            rwv[k] = a.rw[sl * plane + ep];
-            rgv[k] = a.rg[sl * plane + ep];
-        } else {
-            rwv[k] = rgv[k] = -1.0f;                // clip(0) - 1: the reset zeros
+    for (int q = 0; q < kNnAgentPer; ++q) {
+        const int p = base + q * kNnChunk + tid;
+        const int pc = p < a.P ? p : 0;
+        to[q] = th_old[pc];
+        tn[q] = th_new[pc];
+        gp[q] = gpv[pc];
+        g[q] = gnv[pc];
+        row[q] = a.agent_row[pc];
+#pragma unroll
+        for (int k = 1; k < kNnRegH; ++k) {
+            if (k < H && k < s) {                   // block-uniform
+                const size_t sl = ((slot - k) % H + H) % H;
+                rwv[q][k] = rw[sl * plane + pc];
+                rgv[q][k] = rg[sl * plane + pc];
+            } else {
+                rwv[q][k] = rgv[q][k] = -1.0f;      // clip(0) - 1: the reset zeros
+            }
         }
     }
     if (tid < H) {
@@ -658,52 +693,67 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_kernel(NnArgs a) {
         else if (k < s) lk = a.al[(((slot - k) % H + H) % H) * E + e];
         lobs[k] = static_cast<float>(clip100(lk) - 1.0);
     }
-    rows_s[tid] = on ? row : -1;
-
-    const double adj_w = ratio(th_new, th_old);
-    const double adj_g = ratio(g, gp);
-    const float ow = static_cast<float>(clip100(adj_w) - 1.0);
-    const float og = static_cast<float>(clip100(adj_g) - 1.0);
     double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    if (on) {
-        v[0] = fabs(static_cast<double>(th_new));
-        v[1] = fabs(adj_w);
-        v[2] = fabs(adj_g);
-        v[3] = g;
-        v[4] = fabs(static_cast<double>(g) - static_cast<double>(gp));
-        a.rw[slot * plane + ep] = ow;
-        a.rg[slot * plane + ep] = og;
-        if (sc.wipe) a.theta_n[ep] = a.theta0[ep];   // theta_n is current next step
-    }
-    __syncthreads();
-    // ---- the agent's row [w~ (H, newest first) | l~ (H) | g~ (H)] in LDS
-    const int W = 3 * H;
-    float *st = stage + tid * W;
-#pragma unroll
-    for (int k = 0; k < kNnMaxH; ++k) {
-        if (k < H) {
-            const bool reset_row = sc.wipe;
-            st[k] = reset_row ? -1.0f : (k == 0 ? ow : rwv[k]);
-            st[H + k] = reset_row ? -1.0f : lobs[k];
-            st[2 * H + k] = reset_row ? -1.0f : (k == 0 ? og : rgv[k]);
-        }
-    }
-    __syncthreads();
-    // ---- rows out: flat (agent j, entry k) across the block, so a wave's
-    // stores cover whole runs of consecutive rows (consecutive agents are
-    // consecutive rows in sorted-name order within each decade)
-    const int n = (a.P - p0 < kNnChunk ? a.P - p0 : kNnChunk) * W;
     float *obs = a.obs + e * static_cast<size_t>(a.P) * W;
     const int dj = kNnChunk / W, dk = kNnChunk - dj * W;   // uniform step of (j, k)
-    int j = tid / W, k = tid - (tid / W) * W;
-    for (int f = tid; f < n; f += kNnChunk) {
-        obs[static_cast<size_t>(rows_s[j]) * W + k] = stage[f];
-        j += dj;
-        k += dk;
-        if (k >= W) {
-            k -= W;
-            ++j;
+#pragma unroll
+    for (int q = 0; q < kNnAgentPer; ++q) {
+        const int p0 = base + q * kNnChunk;
+        if (p0 >= a.P) break;                       // block-uniform
+        const int p = p0 + tid;
+        const bool on = p < a.P;
+        const double adj_w = nn_ratio(tn[q], to[q]);
+        const double adj_g = nn_ratio(g[q], gp[q]);
+        const float ow = static_cast<float>(clip100(adj_w) - 1.0);
+        const float og = static_cast<float>(clip100(adj_g) - 1.0);
+        if (on) {
+            v[0] += fabs(static_cast<double>(tn[q]));
+            v[1] += fabs(adj_w);
+            v[2] += fabs(adj_g);
+            v[3] += g[q];
+            v[4] += fabs(static_cast<double>(g[q]) - static_cast<double>(gp[q]));
+            a.rw[slot * plane + e * ps + p] = ow;
+            a.rg[slot * plane + e * ps + p] = og;
+            if (sc.wipe) a.theta_n[e * ps + p] = a.theta0[e * ps + p];
         }
+        rows_s[tid] = on ? row[q] : -1;
+        __syncthreads();                            // lobs ready; the last sub-chunk's rows are out
+        float *st = stage + tid * W;
+#pragma unroll
+        for (int k = 0; k < kNnRegH; ++k) {
+            if (k < H) {
+                st[k] = sc.wipe ? -1.0f : (k == 0 ? ow : rwv[q][k]);
+                st[H + k] = sc.wipe ? -1.0f : lobs[k];
+                st[2 * H + k] = sc.wipe ? -1.0f : (k == 0 ? og : rgv[q][k]);
+            }
+        }
+        for (int k = kNnRegH; k < H; ++k) {         // long histories: loaded here
+            float wk = -1.0f, gk = -1.0f;
+            if (k < s && on) {
+                const size_t sl = ((slot - k) % H + H) % H;
+                wk = rw[sl * plane + p];
+                gk = rg[sl * plane + p];
+            }
+            st[k] = sc.wipe ? -1.0f : wk;
+            st[H + k] = sc.wipe ? -1.0f : lobs[k];
+            st[2 * H + k] = sc.wipe ? -1.0f : gk;
+        }
+        __syncthreads();
+        const int n = (a.P - p0 < kNnChunk ? a.P - p0 : kNnChunk) * W;
+        int j = tid / W, k = tid - (tid / W) * W;
+#ifdef CE_NN_DIAG_NOOBS
+        if (n < 0)   // timing diagnostic: no observation stores
+#endif
+        for (int f = tid; f < n; f += kNnChunk) {
+            obs[static_cast<size_t>(rows_s[j]) * W + k] = stage[f];
+            j += dj;
+            k += dk;
+            if (k >= W) {
+                k -= W;
+                ++j;
+            }
+        }
+        __syncthreads();
     }
     nn_block_sum<5, kNnChunk>(v, red);
     if (tid == 0) {

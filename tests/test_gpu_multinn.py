@@ -169,6 +169,19 @@ def test_small_networks_against_oracle(hidden):
         _check_env(ds, hidden, seed, acts[:, i * P:(i + 1) * P], rows, rec, i, 7)
 
 
+def test_long_history_against_oracle():
+    """max_history 10: ring ages past the 8 the agent kernel keeps in
+    registers are loaded at staging time."""
+    ds = _iris()
+    seeds = [4, 8]
+    hidden = (32,)
+    P = 4 * 32 + 32 + 32 * 3 + 3
+    acts = _actions(16, len(seeds), P, 1.0, 2.5, 6)
+    _, rows, rec = _run_engine(ds, hidden, seeds, acts, max_batches=13, H=10)
+    for i, seed in enumerate(seeds):
+        _check_env(ds, hidden, seed, acts[:, i * P:(i + 1) * P], rows, rec, i, 13, H=10)
+
+
 def test_default_network_against_oracle():
     """get_problem('nn') defaults: create_neural_net (256, 256) over the
     iris-shaped set, P = 67,843 agents per env."""
