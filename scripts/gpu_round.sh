@@ -33,3 +33,8 @@ timeout -k 10 400 python bench.py --workload mlp --steps 20 --warmup 4 --cpu-sec
 echo "bench mlp rc=$rc"; tail -1 $OUT/bench_mlp.log | cut -c1-200; fatal $rc
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_mlp -o run --output-format csv -- python3 bench.py --workload mlp --profile-only --steps 10 --warmup 2 > $OUT/prof_mlp.log 2>&1; rc=$?
 echo "rocprof mlp rc=$rc"; fatal $rc
+# MultiOptLRs over the OptimizeNN network
+timeout -k 10 300 python bench.py --workload nn --steps 40 --warmup 4 --cpu-seconds 20 > $OUT/bench_nn.log 2>&1; rc=$?
+echo "bench nn rc=$rc"; tail -1 $OUT/bench_nn.log | cut -c1-200; fatal $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_nn -o nn --output-format csv -- python3 bench.py --workload nn --profile-only --steps 10 --warmup 2 > $OUT/prof_nn.log 2>&1; rc=$?
+echo "rocprof nn rc=$rc"; fatal $rc
