@@ -261,3 +261,48 @@ def test_optvecenv_and_single_env_surface():
     assert isinstance(reward, float) and isinstance(terminal, bool)
     assert info['loss'] is None and set(info) >= {'batch_loss', 'grads_mean', 'episode'}
     env.close()
+
+
+def test_device_path_and_graphs_match_host_path():
+    """step_device / step_many_device (hipGraph of k steps) give the host
+    path's outputs bit for bit; graphs of odd k start at alternating
+    ping-pong parities (captured per parity)."""
+    import torch
+    from custom_envs_amd.multi_engine import NNMultiEngine
+    ds = _iris()
+    kw = dict(data_set=ds, hidden=(64,), max_batches=5, seeds=[7, 8, 9])
+    host = NNMultiEngine(3, **kw)
+    dev = NNMultiEngine(3, **kw)
+    P = host.n_params
+    T = 11
+    acts = _actions(T, 3, P, 1.0, 2.5, 9)
+    host.reset()
+    ref = []
+    for t in range(T):
+        o = host.step(acts[t])
+        ref.append({k: v.copy() for k, v in o.items()})
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    dev.set_stream(stream.cuda_stream)
+    out = dev.alloc_device_outputs()
+    dev.reset_device(out)
+    dacts = torch.from_numpy(acts).cuda()
+    t = 0
+    for k in (1, 3, 3, 1, 3):          # parities 0, 1, 0, 1, 0 at graph starts
+        if k == 1:
+            dev.step_device(dacts[t], out)
+        else:
+            dev.step_many_device(k, dacts[t:], out)
+        torch.cuda.synchronize()
+        t += k
+        got = {n: v.cpu().numpy() for n, v in out.items()}
+        r = ref[t - 1]
+        assert np.array_equal(got['obs'].reshape(r['obs'].shape), r['obs']), t
+        assert np.array_equal(got['reward'], r['reward'])
+        assert np.array_equal(got['done'], r['done'])
+        assert np.array_equal(got['episode_len'], r['episode_len'])
+        np.testing.assert_array_equal(got['info'], r['info'])
+    assert np.array_equal(host.get_state()['theta'], dev.get_state()['theta'])
+    host.close()
+    dev.close()
+
