@@ -37,6 +37,7 @@ struct ce_nn_engine {
     size_t off[5] = {0};
     size_t out_bytes = 0;
     char *d_out = nullptr, *h_out = nullptr;
+    unsigned long long *diag = nullptr;    // CE_DIAG builds: [2][E][kNnStamps]
     bool seeded = false, was_reset = false;
     hipGraphExec_t graph = nullptr;
     int graph_k = 0, graph_parity = 0;
@@ -293,6 +294,10 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     }
     e->out_bytes = off;
     CE_TRY(hipMalloc(&e->d_out, e->out_bytes));
+#ifdef CE_DIAG
+    CE_TRY(hipMalloc(&e->diag, 2 * E * ce::kNnStamps * sizeof(unsigned long long)));
+    a.diag = e->diag;
+#endif
     CE_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_out), e->out_bytes));
     CE_TRY(hipMemset(e->d_out, 0, e->out_bytes));
     std::memset(e->h_out, 0, e->out_bytes);
@@ -330,7 +335,7 @@ void ce_nn_destroy(ce_nn_engine *e) {
                    e->theta0, e->gU, e->loss_b, e->part_u, e->part_c, e->rw, e->rg,
                    e->al, e->sw, e->sg, e->hl, e->hsg, e->step, e->cursor,
                    e->order, e->order_sel, e->reset_perm, e->epoch_perm, e->agent_row,
-                   e->d_act, e->d_out};
+                   e->d_act, e->d_out, e->diag};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
@@ -461,6 +466,19 @@ int ce_nn_host_outputs(ce_nn_engine *e, ce_multi_outputs *view) {
     *view = region(e, e->h_out);
     return CE_OK;
 }
+
+#ifdef CE_DIAG
+// Diagnostic builds only (not part of include/custom_envs_amd.h): the eval
+// kernels' phase stamps, [2 kernels][E][kNnStamps].
+int ce_nn_diag_stamps(ce_nn_engine *e, unsigned long long *out) {
+    if (!e || !out) return fail(CE_EINVAL, "null argument");
+    CE_HIP(hipStreamSynchronize(e->stream));
+    CE_HIP(hipMemcpy(out, e->diag,
+                     2 * sizeof(unsigned long long) * e->cfg.num_envs * ce::kNnStamps,
+                     hipMemcpyDeviceToHost));
+    return CE_OK;
+}
+#endif
 
 int ce_nn_get_state(ce_nn_engine *e, float *theta, float *gprev, int32_t *step, int32_t *cursor,
                     int32_t *order) {

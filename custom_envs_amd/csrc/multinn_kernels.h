@@ -115,7 +115,35 @@ struct NnArgs {
     uint8_t *done;                 // [E][P] rows
     float *info;                   // [E][14]
     int32_t *episode_len;          // [E]
+    unsigned long long *diag;      // [E][kNnStamps] phase stamps (CE_DIAG builds only)
 };
+
+// Diagnostic builds (-DCE_DIAG) stamp s_memtime (thread 0 of each eval
+// workgroup) at phase boundaries; product builds compile the stamps away.
+constexpr int kNnStamps = 10;
+#ifdef CE_DIAG
+#define NN_STAMP(a, e, k)                                                              \
+    do {                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        unsigned long long t_;                                                         \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        if (threadIdx.x == 0) (a).diag[(e) * kNnStamps + (k)] = t_;                    \
+    } while (0)
+#define NN_STAMP_RT(a, e, k)                                                           \
+    do {                                                                               \
+        unsigned long long t_;                                                         \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+        if (threadIdx.x == 0) (a).diag[(e) * kNnStamps + (k)] = t_;                    \
+    } while (0)
+#else
+#define NN_STAMP(a, e, k) \
+    do {                  \
+    } while (0)
+#define NN_STAMP_RT(a, e, k) \
+    do {                     \
+    } while (0)
+#endif
 
 __device__ __forceinline__ int nn_ld(int w) { return ((w + 31) & ~31) + kNnPad; }
 
@@ -176,21 +204,28 @@ __device__ void nn_forward_hidden(const float *W, const float *bias, int w_in, i
         nn_f32x16 acc = {};
         const float *xrow = in + li * ld_in + 4 * h;
         // W fragments stream from HBM kNnPrefetch chunks ahead (a register
-        // ring refilled right after use); the X rows come from LDS at use
+        // ring refilled right after use); the X rows come from LDS at use.
+        // Loads are branch-free (clamped address, value selected) so the
+        // compiler keeps them all in flight instead of fencing each chunk.
         float wb[kNnPrefetch][4];
+        const int kmax = w_in - 1, clast = c1 - 1;
         auto loadw = [&](int c, float (&w)[4]) {
+            const int cc = c < clast ? c : clast;
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                const int k = 8 * c + 4 * h + m;
-                w[m] = (c < c1 && k < w_in) ? W[static_cast<size_t>(k) * w_out + j] : 0.0f;
+                const int k = 8 * cc + 4 * h + m;
+                const float v = W[static_cast<size_t>(k < kmax ? k : kmax) * w_out + j];
+                w[m] = k <= kmax ? v : 0.0f;
             }
         };
+        if (c0 < c1) {
 #pragma unroll
-        for (int d = 0; d < kNnPrefetch; ++d) loadw(c0 + d, wb[d]);
+            for (int d = 0; d < kNnPrefetch; ++d) loadw(c0 + d, wb[d]);
+        }
         for (int c = c0; c < c1; c += kNnPrefetch) {
 #pragma unroll
             for (int d = 0; d < kNnPrefetch; ++d) {
-                if (c + d < c1) {
+                if (c + d < c1) {                   // uniform
                     const float4 x = *reinterpret_cast<const float4 *>(xrow + 8 * (c + d));
                     acc = nn_mfma(wb[d][0], x.x, acc);
                     acc = nn_mfma(wb[d][1], x.y, acc);
@@ -363,6 +398,7 @@ __device__ __forceinline__ void nn_backward(const NnArgs &a, const float *theta,
         __syncthreads();
     }
 
+    NN_STAMP(a, blockIdx.x, 5);
     // ---- hidden layers l = L-1 .. 0 (layer l maps dims[l] -> dims[l+1]);
     // dZ of its output sits in buffer h[l]
     for (int l = L - 1; l >= 0; --l) {
@@ -372,6 +408,7 @@ __device__ __forceinline__ void nn_backward(const NnArgs &a, const float *theta,
         float *hin = lds + (l ? a.lds_h[l - 1] : a.lds_x);
         const int ldi = nn_ld(w_in);
         const float *W = theta + a.off_w[l];
+        if (l == 0 && L > 1) NN_STAMP(a, blockIdx.x, 6);
 
         // db_l
         for (int j = tid; j < w_out; j += kNnBlock) {
@@ -392,15 +429,17 @@ __device__ __forceinline__ void nn_backward(const NnArgs &a, const float *theta,
                 if (tile < tin) {
                     const float *wrow = W + static_cast<size_t>(tile * 32 + li) * w_out + 4 * h;
                     const float *zrow = dz + li * ldo + 4 * h;
+                    // float4 W rows kNnPrefetch chunks ahead, branch-free
+                    // (clamped addresses) so every load stays in flight
                     float4 wb[kNnPrefetch];
+                    const int clast = chunks - 1;
 #pragma unroll
                     for (int d = 0; d < kNnPrefetch; ++d)
-                        wb[d] = d < chunks ? *reinterpret_cast<const float4 *>(wrow + 8 * d)
-                                           : float4{0.0f, 0.0f, 0.0f, 0.0f};
+                        wb[d] = *reinterpret_cast<const float4 *>(wrow + 8 * (d < clast ? d : clast));
                     for (int c = 0; c < chunks; c += kNnPrefetch) {
 #pragma unroll
                         for (int d = 0; d < kNnPrefetch; ++d) {
-                            if (c + d < chunks) {
+                            if (c + d < chunks) {       // uniform
                                 const float4 zv =
                                     *reinterpret_cast<const float4 *>(zrow + 8 * (c + d));
                                 acc = nn_mfma(wb[d].x, zv.x, acc);
@@ -409,8 +448,7 @@ __device__ __forceinline__ void nn_backward(const NnArgs &a, const float *theta,
                                 acc = nn_mfma(wb[d].w, zv.w, acc);
                             }
                             const int cn = c + kNnPrefetch + d;
-                            if (cn < chunks)
-                                wb[d] = *reinterpret_cast<const float4 *>(wrow + 8 * cn);
+                            wb[d] = *reinterpret_cast<const float4 *>(wrow + 8 * (cn < clast ? cn : clast));
                         }
                     }
                 }
@@ -473,11 +511,13 @@ __device__ float nn_forward(const NnArgs &a, const float *theta, float *lds, con
         lds[a.lds_wo + i] = theta[a.off_w[L] + i];
     for (int l = 0; l < L; ++l) {
         const float *in = lds + (l ? a.lds_h[l - 1] : a.lds_x);
+        if (l == 1) NN_STAMP(a, blockIdx.x, 2);
         nn_forward_hidden(theta + a.off_w[l], theta + a.off_b[l], a.dims[l], a.dims[l + 1], in,
                           nn_ld(a.dims[l]), lds + a.lds_h[l], nn_ld(a.dims[l + 1]),
                           lds + a.lds_part);
         __syncthreads();
     }
+    NN_STAMP(a, blockIdx.x, 3);
     const float *hl = lds + (L ? a.lds_h[L - 1] : a.lds_x);
     nn_forward_logits(lds + a.lds_wo, theta + a.off_b[L], a.dims[L], a.K, hl,
                       nn_ld(a.dims[L]), lds + a.lds_z, nn_ld(a.K));
@@ -520,11 +560,17 @@ struct NnStore {
 
 __device__ __forceinline__ float nn_eval(const NnArgs &a, size_t e, const float *theta, float *g,
                                          float *lds, int *rows, float *red) {
+    NN_STAMP_RT(a, e, 8);
+    NN_STAMP(a, e, 0);
     const int nrows = nn_stage_batch(a, e, lds, rows);
     __syncthreads();
+    NN_STAMP(a, e, 1);
     const float loss = nn_forward(a, theta, lds, rows, nrows, red);
+    NN_STAMP(a, e, 4);
     NnStore st{g};
     nn_backward(a, theta, lds, st);
+    NN_STAMP(a, e, 7);
+    NN_STAMP_RT(a, e, 9);
     return loss;
 }
 
@@ -547,7 +593,11 @@ __global__ __launch_bounds__(kNnBlock, 4) void nn_step_kernel(NnArgs a) {
     __shared__ int rows[kNnBatch];
     __shared__ float red[4];
     const size_t e = blockIdx.x, ps = a.Ps;
-    const float loss = nn_eval(a, e, a.theta_n + e * ps, a.gN + e * ps, lds, rows, red);
+    NnArgs b = a;
+#ifdef CE_DIAG
+    b.diag = a.diag + static_cast<size_t>(a.E) * kNnStamps;   // the step kernel's own record
+#endif
+    const float loss = nn_eval(b, e, a.theta_n + e * ps, a.gN + e * ps, lds, rows, red);
     if (threadIdx.x == 0) a.loss_b[e] = loss;
 }
 
