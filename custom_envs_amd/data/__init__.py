@@ -72,10 +72,23 @@ LOADERS = {
 }
 
 
-def load_data(name='gaussians_256x10', batch_size=32, num_of_labels=None):
-    """Return an ``InMemoryDataSet`` (load_data.py:47-112 signature)."""
+def load_data(name='gaussians_256x10', batch_size=32, num_of_labels=None, data_dir=None):
+    """Return an ``InMemoryDataSet`` (load_data.py:47-112 signature).
+
+    The file-backed sets ('mnist', 'mnist-test', 'fashion', 'emnist-digits',
+    'iris', 'skin'; custom_envs_amd/data/files.py) read ``data_dir``, laid out
+    as the reference's custom_envs/data/ directory; the reference's own copies
+    are git-LFS pointers and are refused.  'cifar-10' needs a keras download
+    and is not served."""
+    from custom_envs_amd.data import files
+    if name in files.IDX_SETS + files.TABLE_SETS:
+        if data_dir is None:
+            raise RuntimeError('data set %r reads files: pass data_dir (the reference ships '
+                               'them as git-LFS pointers)' % name)
+        load = files.load_idx_set if name in files.IDX_SETS else files.load_table_set
+        features, targets = load(data_dir, name, num_of_labels, normalize, to_onehot)
+        return InMemoryDataSet(features, targets, batch_size)
     if name not in LOADERS:
-        raise RuntimeError('No such data set named: {} (real-data loaders are out of '
-                           'scope: the reference ships them as git-LFS pointers)'.format(name))
+        raise RuntimeError('No such data set named: {}'.format(name))
     features, targets = LOADERS[name](num_of_labels)
     return InMemoryDataSet(features, targets, batch_size)
