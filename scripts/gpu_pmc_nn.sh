@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 ARGS="--workload nn --envs ${NN_ENVS:-512} --profile-only --steps 6 --warmup 2"
 i=0
 for CTRS in "FETCH_SIZE" "WRITE_SIZE" \
-            "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES"; do
+            "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $CTRS -d $OUT/p$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1; rc=$?
   echo "pass $i rc=$rc"
