@@ -1,18 +1,30 @@
 """Benchmark: vectorised Optimize-v0 env-steps/s on MI355X (BASELINE.json metric).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--precision f64|f32]
-                  [--workload optimize|multi] [--gather]
+                  [--workload optimize|multi|mlp|nn] [--no-gather]
 
 One "step" = one VecEnv.step of every env: the fused HIP kernel advances
 E = 4096 envs per GPU (weak scaling: N GPUs own N*4096 envs, contiguous
 shards, seed = global env index) of the 256x10 softmax-regression problem by
 one Optimize-v0 step, auto-reset included.  Actions are device-resident
 ([S][E][P] float32 in HBM, a different action block per step) and the
-outputs (obs/reward/done/info) are written to HBM every step.  Steps are
-replayed as hipGraphs of S consecutive launches (ce_step_many).  Envs are
-independent, so there is no data-path collective; ``--gather`` adds the
-north star's RCCL all-gather of the packed outputs every step (config 4,
-custom_envs_amd/distributed.py), reported as its own line.
+outputs (obs/reward/done/info) are written to HBM every step.
+
+Launch.  ``--gpus N`` with N > 1 and no WORLD_SIZE in the environment starts
+``torch.distributed.run`` with N ranks (one process per GPU, RCCL) as a
+child process before anything touches a GPU; under torchrun (the driver's
+launch) the ranks come from RANK/WORLD_SIZE.
+
+Multi-GPU (config 4).  Every step all-gathers the packed outputs of every
+rank (custom_envs_amd/distributed.py: ONE all_gather_into_tensor of a
+256-B-aligned [obs|reward|done|objective|accuracy|len] record per env,
+RCCL over xGMI).  ``value`` is the pipelined form: two output buffers, the
+collective of step t runs on RCCL's stream while step t+1's kernel writes
+the other buffer (the learner consumes step t's global outputs one step
+behind the envs).  The line also carries ``value_gather_serial`` (kernel,
+then the collective, every step: a closed-loop learner) and
+``value_no_gather`` (the env kernels alone, hipGraph replay).  At N = 1 the
+gather is the identity and ``value`` is the hipGraph replay of S steps.
 
 ``--workload multi`` measures config 5 instead: MultiOptLRs-v0 (4 agents,
 4-D Rosenbrock pairs, H=5, max_batches=400) behind OptVecEnv, 1024 envs per
@@ -20,8 +32,8 @@ GPU, actions uniform(1, 3) as in SURVEY 8d.  ``--workload mlp`` measures
 config 3: Optimize-v0 over the 784 -> 64 -> 10 MLP on 1024 MNIST-sized
 synthetic rows, B = 32, 4096 envs, float32 on MFMA (roofline bound "mfma").
 
-Rank 0 prints ONE JSON line.  With N>1 run under
-``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
+Rank 0 prints ONE JSON line.  ``--dry-run`` exercises the launcher and the
+rank protocol on CPU (gloo, no engine) for the tests.
 """
 import argparse
 import json
@@ -102,7 +114,7 @@ def nn_flops_per_env_step(dims):
     return 2 * one
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=2000)
@@ -112,15 +124,43 @@ def parse():
     p.add_argument('--workload', default='optimize', choices=['optimize', 'multi', 'mlp', 'nn'])
     p.add_argument('--precision', default='f64', choices=['f64', 'f32'])
     p.add_argument('--graph-steps', type=int, default=250, help='steps per hipGraph replay')
-    p.add_argument('--gather', action='store_true', help='all-gather outputs every step')
-    p.add_argument('--cpu-seconds', type=float, default=15.0, help='CPU baseline budget')
+    p.add_argument('--no-gather', action='store_true',
+                   help='N > 1: no per-step all-gather in the headline value')
+    p.add_argument('--gather', action='store_true',
+                   help='all-gather every step also for the multi workload')
+    p.add_argument('--cpu-seconds', type=float, default=12.0, help='CPU baseline budget per leg')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--cpu-baseline-only', action='store_true', help=argparse.SUPPRESS)
+    p.add_argument('--force-gather', action='store_true',
+                   help='run the gather modes at world 1 too (a real 1-rank RCCL collective)')
+    p.add_argument('--dry-run', action='store_true',
+                   help='launcher + rank protocol only (gloo on CPU, no engine)')
     p.add_argument('--profile-only', action='store_true',
                    help='run the timed steps only (for rocprofv3)')
-    args = p.parse_args()
+    args = p.parse_args(argv)
     if args.envs is None:
         args.envs = {'multi': 1024, 'nn': 1024}.get(args.workload, 4096)
     return args
+
+
+def _free_port():
+    import socket
+    with socket.socket() as sock:
+        sock.bind(('127.0.0.1', 0))
+        return sock.getsockname()[1]
+
+
+def launch_ranks(args):
+    """``--gpus N`` without a torchrun environment: run this script under
+    ``torch.distributed.run`` with N ranks as a CHILD process (this process
+    has not touched a GPU and never execs) and return its exit code."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.call(cmd, env=env)
 
 
 def lr_dataset():
@@ -146,35 +186,87 @@ def _time_cpu(venv, acts, budget_s):
         venv.step(acts)
         steps += 1
         wall = time.perf_counter() - wall0
-        if wall >= budget_s or steps >= 1000:
+        if wall >= budget_s or steps >= 100000:
             break
     return steps, wall, time.process_time() - cpu0
 
 
+def host_info():
+    """What the CPU numbers ran on: model, cores, BLAS threads."""
+    model = None
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for line in fh:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return {'cpu_model': model, 'os_cpu_count': os.cpu_count(), 'affinity_cpus': affinity,
+            'blas_threads': {k: os.environ.get(k) for k in
+                             ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS')},
+            'ulimit_n': resource.getrlimit(resource.RLIMIT_NOFILE)[0],
+            'numpy': np.__version__}
+
+
+def cpu_share():
+    """Worker processes the box grants this job (16 CPUs per GPU there;
+    os.cpu_count() reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+def _optimize_factory(features, targets, seed):
+    def make():
+        from oracle.optimize import Optimize as OracleEnv
+        env = OracleEnv(features, targets)
+        env.seed(seed)
+        return env
+    return make
+
+
 def cpu_baseline(features, targets, envs, budget_s):
-    """The reference's NumPy path restated: oracle envs under ThreadVecEnv."""
-    from oracle.optimize import Optimize as OracleEnv
-    from oracle.vectorize import ThreadVecEnv
+    """The reference's NumPy path restated: oracle envs under the restated
+    custom_envs.vectorize (concurrentvecenv.py:64-268), two legs:
+    ThreadVecEnv at the GPU's env count (one thread + mp.Pipe per env, the
+    reference's configuration) and SubprocVecEnv with one process per CPU
+    of this job's share.  ``value`` is the faster leg."""
+    from oracle.vectorize import SubprocVecEnv, ThreadVecEnv
     n = _raise_fd_limit(envs)
-
-    def factory(seed):
-        def make():
-            env = OracleEnv(features, targets)
-            env.seed(seed)
-            return env
-        return make
-
-    venv = ThreadVecEnv([factory(i) for i in range(n)])
+    venv = ThreadVecEnv([_optimize_factory(features, targets, i) for i in range(n)])
     venv.reset()
     acts = np.random.RandomState(0).normal(0, 0.01, (n, 20)).astype(np.float32)
     steps, wall, cpu = _time_cpu(venv, acts, budget_s)
     venv.close()
-    return {'value': n * steps / wall, 'unit': 'env-steps/s',
-            'cores': max(1, int(round(cpu / wall))), 'kind': 'port',
-            'sample': '%d envs x %d steps of ThreadVecEnv (1 thread + mp.Pipe per env, '
-                      'pickled step msgs, np.stack) over the float64 numpy oracle '
-                      'Optimize env; %.1f s wall, %.1f s CPU; os.cpu_count()=%d'
-                      % (n, steps, wall, cpu, os.cpu_count())}
+    thread = {'value': n * steps / wall, 'envs': n, 'steps': steps, 'wall_s': wall,
+              'cpu_s': cpu, 'cores': max(1, int(round(cpu / wall)))}
+    p = cpu_share()
+    venv = SubprocVecEnv([_optimize_factory(features, targets, i) for i in range(p)], 'fork')
+    venv.reset()
+    acts = np.random.RandomState(0).normal(0, 0.01, (p, 20)).astype(np.float32)
+    steps, wall, _ = _time_cpu(venv, acts, budget_s)
+    venv.close()
+    sub = {'value': p * steps / wall, 'envs': p, 'steps': steps, 'wall_s': wall, 'cores': p}
+    best = max((thread, 'ThreadVecEnv'), (sub, 'SubprocVecEnv'), key=lambda x: x[0]['value'])
+    return {'value': best[0]['value'], 'unit': 'env-steps/s', 'cores': best[0]['cores'],
+            'kind': 'port',
+            'sample': ('%s leg (the faster of two): ThreadVecEnv %d envs x %d steps '
+                       '(1 thread + mp.Pipe per env, pickled step msgs, np.stack; %.1f s wall) '
+                       '= %.3g env-steps/s; SubprocVecEnv %d processes x %d steps (%.1f s '
+                       'wall) = %.3g env-steps/s; both over the float64 numpy oracle '
+                       'Optimize env, 256x10, B=N' % (
+                           best[1], thread['envs'], thread['steps'], thread['wall_s'],
+                           thread['value'], sub['envs'], sub['steps'], sub['wall_s'],
+                           sub['value'])),
+            'legs': {'ThreadVecEnv': thread, 'SubprocVecEnv': sub},
+            'host': host_info()}
 
 
 def cpu_baseline_multi(envs, budget_s):
@@ -305,16 +397,109 @@ def cpu_baseline_nn(budget_s):
                       'os.cpu_count()=%d' % (n, steps, wall, cpu, os.cpu_count())}
 
 
+def run_cpu_baseline_child(args):
+    """The CPU legs in a child process started before this process touches
+    the GPU (SubprocVecEnv forks workers; nothing forks from a GPU process)."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), '--cpu-baseline-only',
+           '--workload', args.workload, '--envs', str(args.envs),
+           '--cpu-seconds', str(args.cpu_seconds)]
+    res = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    for line in reversed(res.stdout.splitlines()):
+        if line.startswith('{'):
+            return json.loads(line)
+    return {'value': None, 'error': 'cpu baseline child failed rc=%d: %s'
+            % (res.returncode, res.stderr[-500:])}
+
+
+def cpu_baseline_only(args):
+    if args.workload == 'nn':
+        cpu = cpu_baseline_nn(args.cpu_seconds)
+    elif args.workload == 'multi':
+        cpu = cpu_baseline_multi(args.envs, args.cpu_seconds)
+    elif args.workload == 'mlp':
+        cpu = cpu_baseline_mlp(args.envs, args.cpu_seconds)
+    else:
+        cpu = cpu_baseline(*lr_dataset(), args.envs, args.cpu_seconds)
+    cpu.setdefault('host', host_info())
+    print(json.dumps(cpu))
+
+
+def dry_run(args, world, rank):
+    """The rank protocol without an engine: gloo, barrier + max-over-ranks
+    timing of K no-op steps; rank 0 prints the line with n_gpus = world."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group('gloo')
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({'metric': METRIC, 'value': None, 'n_gpus': world, 'steps': args.steps,
+                          'warmup': args.warmup, 'dry_run': True, 'elapsed_s': elapsed,
+                          'world_size_env': os.environ.get('WORLD_SIZE')}))
+
+
+def _timed(torch, dist, fn, steps):
+    """barrier + synchronize on both sides of exactly `steps` steps; the max
+    over ranks."""
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn(steps)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def main():
     args = parse()
-    import torch
+    if args.cpu_baseline_only:
+        cpu_baseline_only(args)
+        return 0
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        return launch_ranks(args)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        print('bench: --gpus %d but WORLD_SIZE=%d; measuring %d ranks'
+              % (args.gpus, world, world), file=sys.stderr)
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return 0
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
+        cpu = run_cpu_baseline_child(args)     # before this process touches the GPU
+
+    import torch
     dist = None
-    if world > 1:
+    if world > 1 or args.force_gather:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
+        if world == 1:
+            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+            os.environ.setdefault('MASTER_PORT', str(_free_port()))
+            os.environ.setdefault('RANK', '0')
+            os.environ.setdefault('WORLD_SIZE', '1')
         dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
     else:
         torch.cuda.set_device(0)
@@ -329,47 +514,78 @@ def main():
     stream = torch.cuda.Stream()          # a real stream: graphs cannot capture the null stream
     torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
+    gather_modes = (world > 1 or args.force_gather) and not args.no_gather and (
+        args.workload == 'optimize' or (multi and args.gather))
     shard = None
-    if args.gather and dist is not None:
+    if gather_modes:
         from custom_envs_amd.distributed import ShardedEnvs
-        shard = ShardedEnvs(eng, world * E, rank, world)
-        out = shard.out                   # the engine writes straight into the packed buffer
+        # two packed buffers: the engine writes straight into them (no packing kernels)
+        shard = ShardedEnvs(eng, world * E, rank, world, slots=2, collective=True)
+        out = shard.outs[0]
     else:
         out = eng.alloc_device_outputs()
     eng.reset_device(out)
 
-    def run(k):
-        done = 0
-        while done < k:
-            n = min(S, k - done)
-            if shard is None:
-                eng.step_many_device(n, actions, out)
-            else:
-                for s in range(n):
-                    eng.step_device(actions[s], out)
-                    shard.gather()
-            done += n
+    def chunks(k):
+        sizes = [S] * (k // S) + ([k % S] if k % S else [])
+        return sizes
 
-    run(args.warmup)
-    torch.cuda.synchronize()
+    def run_graph(k):
+        for n in chunks(k):
+            eng.step_many_device(n, actions, out)
+
+    pending = [None, None]
+    counter = [0]
+
+    def run_gather_pipelined(k):
+        # step t writes slot t % 2; its all-gather runs on RCCL's stream while
+        # step t+1 writes the other slot; before a slot is rewritten, the
+        # engine stream waits for the collective that read it
+        for _ in range(k):
+            t = counter[0]
+            slot = t & 1
+            if pending[slot] is not None:
+                pending[slot].wait()
+            eng.step_device(actions[t % S], shard.outs[slot])
+            _, pending[slot] = shard.gather(slot, async_op=True)
+            counter[0] += 1
+        for slot in (0, 1):
+            if pending[slot] is not None:
+                pending[slot].wait()
+                pending[slot] = None
+
+    def run_gather_serial(k):
+        for _ in range(k):
+            t = counter[0]
+            eng.step_device(actions[t % S], shard.outs[0])
+            shard.gather(0)
+            counter[0] += 1
+
+    # hipGraphs for every chunk size the graph mode replays, built before any timing
+    for n in sorted(set(chunks(args.warmup) + chunks(args.steps))):
+        eng.prepare_many_device(n, actions, out)
     if args.profile_only:
-        run(args.steps)
+        run_graph(args.warmup)
         torch.cuda.synchronize()
-        return
+        run_graph(args.steps)
+        torch.cuda.synchronize()
+        return 0
 
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    modes = {}
+    if gather_modes:
+        primary = run_gather_pipelined
+        run_gather_pipelined(args.warmup)
+        modes['pipelined'] = _timed(torch, dist, run_gather_pipelined, args.steps)
+        run_gather_serial(args.warmup)
+        modes['serial'] = _timed(torch, dist, run_gather_serial, args.steps)
+        run_graph(args.warmup)
+        modes['no_gather'] = _timed(torch, dist, run_graph, args.steps)
+        elapsed = modes['pipelined']
+    else:
+        primary = run_graph
+        primary(args.warmup)
+        torch.cuda.synchronize()
+        elapsed = _timed(torch, dist, primary, args.steps)
 
     # live kernel duration: HIP events on the engine's stream (= torch's
     # current stream) around graph replays of S back-to-back step launches,
@@ -385,7 +601,7 @@ def main():
         eng.step_many_device(S, actions, out)
         ends[i].record(stream)
     torch.cuda.synchronize()
-    times = [s.elapsed_time(e) / S for s, e in zip(starts, ends)]
+    times = [a.elapsed_time(b) / S for a, b in zip(starts, ends)]
     kernel_ms, kernel_ms_mean = float(np.median(times)), float(np.mean(times))
     phase_ms = {}
     if mlp and rank == 0:
@@ -412,16 +628,6 @@ def main():
     host_rate = None
     if rank == 0 and world == 1 and args.workload == 'optimize':
         host_rate = host_loop_rate(args, device, E)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if nn:
-            cpu = cpu_baseline_nn(args.cpu_seconds)
-        elif multi:
-            cpu = cpu_baseline_multi(E, args.cpu_seconds)
-        elif mlp:
-            cpu = cpu_baseline_mlp(E, args.cpu_seconds)
-        else:
-            cpu = cpu_baseline(*lr_dataset(), E, args.cpu_seconds)
 
     if rank == 0:
         if mlp:
@@ -432,6 +638,12 @@ def main():
         else:
             line = (multi_line if multi else optimize_line)(args, eng, world, E, S, elapsed,
                                                             kernel_ms, kernel_ms_mean, shard)
+        if modes:
+            units = world * E * args.steps
+            line['value_gather_serial'] = units / modes['serial']
+            line['value_no_gather'] = units / modes['no_gather']
+            line['ms_per_step_modes'] = {k: v / args.steps * 1e3 for k, v in modes.items()}
+            line['gather_bytes_per_rank'] = shard.layout.nbytes
         line['cpu_baseline'] = cpu
         if host_rate is not None:
             line['host_loop_env_steps_per_s'] = host_rate
@@ -439,6 +651,7 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 def host_loop_rate(args, device, E):
@@ -507,7 +720,8 @@ def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, sh
             'envs_per_gpu': E, 'global_envs': world * E, 'n_rows': 256,
             'n_features': 10, 'n_classes': 2, 'batch_size': 256,
             'graph_steps': S, 'parallelism': 'env-sharded x%d (no collective)' % world
-            if shard is None else 'env-sharded x%d + all-gather/step' % world,
+            if shard is None else 'env-sharded x%d + one RCCL all-gather of the packed '
+            'outputs per step, pipelined over 2 buffers' % world,
         },
         'roofline': {
             'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
@@ -543,7 +757,8 @@ def multi_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard
                         'device-resident actions/outputs' % (E, E * P),
             'envs_per_gpu': E, 'global_envs': world * E, 'agents': P, 'max_history': H,
             'graph_steps': S, 'parallelism': 'env-sharded x%d (no collective)' % world
-            if shard is None else 'env-sharded x%d + all-gather/step' % world,
+            if shard is None else 'env-sharded x%d + one RCCL all-gather of the packed '
+            'outputs per step, pipelined over 2 buffers' % world,
         },
         'roofline': {
             'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
@@ -631,4 +846,4 @@ def mlp_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard, 
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

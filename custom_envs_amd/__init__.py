@@ -11,6 +11,8 @@ from custom_envs_amd._native import NativeEngineError
 
 register(id='Optimize-v0', entry_point='custom_envs_amd.envs.optimize:Optimize')
 register(id='MultiOptLRs-v0', entry_point='custom_envs_amd.envs.multioptlrs:MultiOptLRs')
+register(id='MultiOptimize-v0',
+         entry_point='custom_envs_amd.envs.multioptimize:MultiOptimize')
 
 __all__ = ['Env', 'Wrapper', 'make', 'register', 'registry', 'load_data',
            'NativeEngineError']

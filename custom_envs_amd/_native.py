@@ -29,14 +29,16 @@ EXPORTS = (
     'ce_abi_version', 'ce_last_error', 'ce_create', 'ce_destroy', 'ce_set_stream',
     'ce_num_envs', 'ce_obs_dim', 'ce_act_dim', 'ce_seed', 'ce_seed_draws',
     'ce_seed_draws_mlp', 'ce_reset',
-    'ce_step', 'ce_step_async', 'ce_wait', 'ce_step_many', 'ce_host_outputs', 'ce_step_kernel',
+    'ce_step', 'ce_step_async', 'ce_wait', 'ce_step_many', 'ce_step_many_prepare',
+    'ce_host_outputs', 'ce_step_kernel',
     'ce_get_state', 'ce_set_state',
     'ce_multi_create', 'ce_multi_destroy', 'ce_multi_set_stream', 'ce_multi_reset',
     'ce_multi_step', 'ce_multi_step_async', 'ce_multi_wait', 'ce_multi_step_many',
+    'ce_multi_step_many_prepare',
     'ce_multi_host_outputs', 'ce_multi_get_state',
     'ce_nn_create', 'ce_nn_destroy', 'ce_nn_set_stream', 'ce_nn_n_params', 'ce_nn_seed',
     'ce_nn_seed_draws', 'ce_nn_reset', 'ce_nn_step', 'ce_nn_step_async', 'ce_nn_wait',
-    'ce_nn_step_many', 'ce_nn_host_outputs', 'ce_nn_get_state',
+    'ce_nn_step_many', 'ce_nn_step_many_prepare', 'ce_nn_host_outputs', 'ce_nn_get_state',
 )
 
 CE_FUNC_ROSENBROCK_PAIRS = 0
@@ -112,6 +114,7 @@ def _declare(lib):
         'ce_step_async': ([vp, vp, ctypes.POINTER(CeOutputs), u32], ctypes.c_int),
         'ce_wait': ([vp], ctypes.c_int),
         'ce_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeOutputs)], ctypes.c_int),
+        'ce_step_many_prepare': ([vp, i32, vp, i64, ctypes.POINTER(CeOutputs)], ctypes.c_int),
         'ce_host_outputs': ([vp, ctypes.POINTER(CeOutputs)], ctypes.c_int),
         'ce_step_kernel': ([vp], ctypes.c_char_p),
         'ce_get_state': ([vp, ctypes.POINTER(CeState)], ctypes.c_int),
@@ -124,6 +127,8 @@ def _declare(lib):
         'ce_multi_step_async': ([vp, vp, ctypes.POINTER(CeMultiOutputs), u32], ctypes.c_int),
         'ce_multi_wait': ([vp], ctypes.c_int),
         'ce_multi_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
+        'ce_multi_step_many_prepare': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs)],
+                                       ctypes.c_int),
         'ce_multi_host_outputs': ([vp, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
         'ce_multi_get_state': ([vp, vp, vp], ctypes.c_int),
         'ce_nn_create': ([ctypes.POINTER(CeNnConfig), vp, vp, ctypes.POINTER(vp)], ctypes.c_int),
@@ -137,6 +142,8 @@ def _declare(lib):
         'ce_nn_step_async': ([vp, vp, ctypes.POINTER(CeMultiOutputs), u32], ctypes.c_int),
         'ce_nn_wait': ([vp], ctypes.c_int),
         'ce_nn_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
+        'ce_nn_step_many_prepare': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs)],
+                                    ctypes.c_int),
         'ce_nn_host_outputs': ([vp, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
         'ce_nn_get_state': ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
     }

@@ -68,6 +68,7 @@ def _compile(out, tmp, defines, verbose):
     common = ['-O3', '-fPIC', '-std=c++17', '-Wall', '-I', os.path.join(ROOT, 'include')]
     common += ['-D' + d for d in defines]
     os.makedirs(tmp, exist_ok=True)
+    cmds = []
     for src in sources():
         obj = os.path.join(tmp, os.path.basename(src) + '.o')
         if src.endswith('.hip'):
@@ -76,8 +77,13 @@ def _compile(out, tmp, defines, verbose):
             cmd = [hipcc, '-x', 'c++'] + common + ['-c', src, '-o', obj]
         if verbose:
             print(' '.join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        cmds.append(cmd)
         objs.append(obj)
+    # one hipcc per translation unit, in parallel
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(len(cmds), 8)) as pool:
+        for proc in pool.map(lambda c: subprocess.run(c, check=True), cmds):
+            pass
     cmd = [hipcc, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out + '.tmp'] + objs
     subprocess.run(cmd, check=True)
     os.replace(out + '.tmp', out)

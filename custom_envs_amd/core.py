@@ -130,3 +130,24 @@ def make(id, **kwargs):  # noqa: A002
     if id not in registry:
         raise KeyError('unknown environment id %r' % id)
     return registry[id].make(**kwargs)
+
+
+def is_make(func):
+    """True for this package's ``make`` and for ``gym.make``: the agent
+    scripts build env factories as ``partial(gym.make, id, **kw)``
+    (search_optimize_hyperparam.py:100-103, play_optimize.py:106-107), and
+    with gym present the ids registered above resolve to this package."""
+    if func is make:
+        return True
+    module = getattr(func, '__module__', None) or ''
+    return getattr(func, '__name__', None) == 'make' and module.split('.')[0] == 'gym'
+
+
+def make_request(fn):
+    """(env id, kwargs) a factory ``partial(make | gym.make, id, **kw)``
+    stands for, or None."""
+    import functools
+    if (isinstance(fn, functools.partial) and is_make(fn.func) and len(fn.args) == 1
+            and fn.args[0] in registry):
+        return fn.args[0], dict(fn.keywords)
+    return None

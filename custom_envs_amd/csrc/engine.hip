@@ -116,13 +116,7 @@ struct ce_engine {
     StepFn pair = nullptr;    // two-envs-per-wave step kernel, when the shape has one
     std::string kernel_name;  // what ce_step_kernel reports
     size_t stage_bytes = 0;
-    // ce_step_many graph cache
-    hipGraphExec_t graph = nullptr;
-    int graph_k = 0;
-    const float *graph_act = nullptr;
-    int64_t graph_stride = 0;
-    ce_outputs graph_out{};
-    hipStream_t graph_stream = nullptr;
+    ce::GraphCache graphs;   // ce_step_many
     unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
 };
 
@@ -514,7 +508,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
 void ce_destroy(ce_engine *e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    if (e->graph) (void)hipGraphExecDestroy(e->graph);
+    e->graphs.release();
     void *dev[] = {e->X, e->Xs, e->label, e->W, e->G, e->W0, e->L, e->step,
                    e->perm, e->order, e->order_sel, e->d_act, e->d_out, e->diag};
     for (void *p : dev)
@@ -610,37 +604,35 @@ int ce_wait(ce_engine *e) {
     return CE_OK;
 }
 
-int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
-                 const ce_outputs *out) {
+namespace {
+
+int many_graph(ce_engine *e, int32_t k, const float *actions, int64_t stride,
+               const ce_outputs *out, hipGraphExec_t *exec) {
     if (!e) return fail(CE_EINVAL, "null engine");
     if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
     if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "ce_step_many: bad arguments");
     if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
     const ce_outputs o = out ? *out : region_view(e, e->d_out);
-    const bool hit = e->graph && e->graph_k == k && e->graph_act == actions &&
-                     e->graph_stride == stride && e->graph_stream == e->stream &&
-                     std::memcmp(&e->graph_out, &o, sizeof(o)) == 0;
-    if (!hit) {
-        if (e->graph) {
-            CE_HIP(hipGraphExecDestroy(e->graph));
-            e->graph = nullptr;
-        }
-        hipGraph_t g;
-        CE_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+    return e->graphs.get(ce::graph_key(k, 0, actions, stride, e->stream, o), [&] {
         for (int s = 0; s < k; ++s) launch(e, false, actions + s * stride, o, e->stream);
-        CE_HIP(hipStreamEndCapture(e->stream, &g));
-        hipError_t err = hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        if (err != hipSuccess)
-            return fail(CE_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(err));
-        e->graph_k = k;
-        e->graph_act = actions;
-        e->graph_stride = stride;
-        e->graph_out = o;
-        e->graph_stream = e->stream;
-    }
-    CE_HIP(hipGraphLaunch(e->graph, e->stream));
+    }, exec);
+}
+
+}  // namespace
+
+int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
+                 const ce_outputs *out) {
+    hipGraphExec_t exec;
+    const int rc = many_graph(e, k, actions, stride, out, &exec);
+    if (rc != CE_OK) return rc;
+    CE_HIP(hipGraphLaunch(exec, e->stream));
     return CE_OK;
+}
+
+int ce_step_many_prepare(ce_engine *e, int32_t k, const float *actions, int64_t stride,
+                         const ce_outputs *out) {
+    hipGraphExec_t exec;
+    return many_graph(e, k, actions, stride, out, &exec);
 }
 
 const char *ce_step_kernel(const ce_engine *e) {

@@ -65,12 +65,7 @@ struct ce_multi_engine {
     size_t out_bytes = 0;
     char *d_out = nullptr, *h_out = nullptr;
     bool was_reset = false;
-    hipGraphExec_t graph = nullptr;
-    int graph_k = 0;
-    const float *graph_act = nullptr;
-    int64_t graph_stride = 0;
-    ce_multi_outputs graph_out{};
-    hipStream_t graph_stream = nullptr;
+    ce::GraphCache graphs;   // ce_multi_step_many
 };
 
 namespace {
@@ -236,7 +231,7 @@ int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out) {
 void ce_multi_destroy(ce_multi_engine *e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    if (e->graph) (void)hipGraphExecDestroy(e->graph);
+    e->graphs.release();
     void *dev[] = {e->theta, e->grad, e->hl, e->hg, e->hw,
                    e->al, e->ag, e->aw, e->step, e->d_act, e->d_out};
     for (void *p : dev)
@@ -292,38 +287,36 @@ int ce_multi_wait(ce_multi_engine *e) {
     return CE_OK;
 }
 
-int ce_multi_step_many(ce_multi_engine *e, int32_t k, const float *actions, int64_t stride,
-                       const ce_multi_outputs *out) {
+namespace {
+
+int multi_graph(ce_multi_engine *e, int32_t k, const float *actions, int64_t stride,
+                const ce_multi_outputs *out, hipGraphExec_t *exec) {
     if (!e) return fail(CE_EINVAL, "null engine");
     if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
     if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "bad arguments");
     if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
     const ce_multi_outputs o = out ? *out : region(e, e->d_out);
-    const bool hit = e->graph && e->graph_k == k && e->graph_act == actions &&
-                     e->graph_stride == stride && e->graph_stream == e->stream &&
-                     std::memcmp(&e->graph_out, &o, sizeof(o)) == 0;
-    if (!hit) {
-        if (e->graph) {
-            CE_HIP(hipGraphExecDestroy(e->graph));
-            e->graph = nullptr;
-        }
-        hipGraph_t g;
-        CE_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+    return e->graphs.get(ce::graph_key(k, 0, actions, stride, e->stream, o), [&] {
         for (int s = 0; s < k; ++s)
             e->kern->step(make_args(e, actions + s * stride, o), grid_of(e), e->stream);
-        CE_HIP(hipStreamEndCapture(e->stream, &g));
-        hipError_t err = hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        if (err != hipSuccess)
-            return fail(CE_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(err));
-        e->graph_k = k;
-        e->graph_act = actions;
-        e->graph_stride = stride;
-        e->graph_out = o;
-        e->graph_stream = e->stream;
-    }
-    CE_HIP(hipGraphLaunch(e->graph, e->stream));
+    }, exec);
+}
+
+}  // namespace
+
+int ce_multi_step_many(ce_multi_engine *e, int32_t k, const float *actions, int64_t stride,
+                       const ce_multi_outputs *out) {
+    hipGraphExec_t exec;
+    const int rc = multi_graph(e, k, actions, stride, out, &exec);
+    if (rc != CE_OK) return rc;
+    CE_HIP(hipGraphLaunch(exec, e->stream));
     return CE_OK;
+}
+
+int ce_multi_step_many_prepare(ce_multi_engine *e, int32_t k, const float *actions,
+                               int64_t stride, const ce_multi_outputs *out) {
+    hipGraphExec_t exec;
+    return multi_graph(e, k, actions, stride, out, &exec);
 }
 
 int ce_multi_host_outputs(ce_multi_engine *e, ce_multi_outputs *view) {

@@ -39,12 +39,7 @@ struct ce_nn_engine {
     char *d_out = nullptr, *h_out = nullptr;
     unsigned long long *diag = nullptr;    // CE_DIAG builds: [2][E][kNnStamps]
     bool seeded = false, was_reset = false;
-    hipGraphExec_t graph = nullptr;
-    int graph_k = 0, graph_parity = 0;
-    const float *graph_act = nullptr;
-    int64_t graph_stride = 0;
-    ce_multi_outputs graph_out{};
-    hipStream_t graph_stream = nullptr;
+    ce::GraphCache graphs;   // ce_nn_step_many
 };
 
 namespace {
@@ -330,7 +325,7 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
 void ce_nn_destroy(ce_nn_engine *e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    if (e->graph) (void)hipGraphExecDestroy(e->graph);
+    e->graphs.release();
     void *dev[] = {e->X, e->label, e->theta_buf[0], e->theta_buf[1], e->g_buf[0], e->g_buf[1],
                    e->theta0, e->gU, e->loss_b, e->part_u, e->part_c, e->rw, e->rg,
                    e->al, e->sw, e->sg, e->hl, e->hsg, e->step, e->cursor,
@@ -378,9 +373,16 @@ int ce_nn_seed(ce_nn_engine *e, const uint64_t *seeds, int32_t n) {
         });
     }
     for (auto &t : pool) t.join();
-    CE_HIP(hipMemcpy(e->theta0, th.data(), E * Ps * sizeof(float), hipMemcpyHostToDevice));
-    CE_HIP(hipMemcpy(e->reset_perm, rp.data(), E * N * sizeof(int32_t), hipMemcpyHostToDevice));
-    CE_HIP(hipMemcpy(e->epoch_perm, ep.data(), E * N * sizeof(int32_t), hipMemcpyHostToDevice));
+    // stream-ordered after any step still reading theta0 / the permutations
+    // (the engine stream is non-blocking, so null-stream copies would race)
+    CE_HIP(hipStreamSynchronize(e->stream));
+    CE_HIP(hipMemcpyAsync(e->theta0, th.data(), E * Ps * sizeof(float), hipMemcpyHostToDevice,
+                          e->stream));
+    CE_HIP(hipMemcpyAsync(e->reset_perm, rp.data(), E * N * sizeof(int32_t),
+                          hipMemcpyHostToDevice, e->stream));
+    CE_HIP(hipMemcpyAsync(e->epoch_perm, ep.data(), E * N * sizeof(int32_t),
+                          hipMemcpyHostToDevice, e->stream));
+    CE_HIP(hipStreamSynchronize(e->stream));
     e->seeded = true;
     return CE_OK;
 }
@@ -423,8 +425,10 @@ int ce_nn_wait(ce_nn_engine *e) {
     return CE_OK;
 }
 
-int ce_nn_step_many(ce_nn_engine *e, int32_t k, const float *actions, int64_t stride,
-                    const ce_multi_outputs *out) {
+namespace {
+
+int nn_graph(ce_nn_engine *e, int32_t k, const float *actions, int64_t stride,
+             const ce_multi_outputs *out, hipGraphExec_t *exec) {
     if (!e) return fail(CE_EINVAL, "null engine");
     if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
     if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "bad arguments");
@@ -432,33 +436,29 @@ int ce_nn_step_many(ce_nn_engine *e, int32_t k, const float *actions, int64_t st
     const ce_multi_outputs o = out ? *out : region(e, e->d_out);
     // the captured launches bake in the ping-pong pointers of their parity
     const int p0 = e->parity;
-    const bool hit = e->graph && e->graph_k == k && e->graph_act == actions &&
-                     e->graph_stride == stride && e->graph_stream == e->stream &&
-                     e->graph_parity == p0 && std::memcmp(&e->graph_out, &o, sizeof(o)) == 0;
-    if (!hit) {
-        if (e->graph) {
-            CE_HIP(hipGraphExecDestroy(e->graph));
-            e->graph = nullptr;
-        }
-        hipGraph_t g;
-        CE_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = e->graphs.get(ce::graph_key(k, p0, actions, stride, e->stream, o), [&] {
         for (int s = 0; s < k; ++s) launch_step(e, actions + s * stride, o, e->stream);
-        e->parity = p0;
-        CE_HIP(hipStreamEndCapture(e->stream, &g));
-        hipError_t err = hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        if (err != hipSuccess)
-            return fail(CE_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(err));
-        e->graph_k = k;
-        e->graph_act = actions;
-        e->graph_stride = stride;
-        e->graph_out = o;
-        e->graph_stream = e->stream;
-        e->graph_parity = p0;
-    }
-    CE_HIP(hipGraphLaunch(e->graph, e->stream));
-    e->parity = p0 ^ (k & 1);
+    }, exec);
+    e->parity = p0;
+    return rc;
+}
+
+}  // namespace
+
+int ce_nn_step_many(ce_nn_engine *e, int32_t k, const float *actions, int64_t stride,
+                    const ce_multi_outputs *out) {
+    hipGraphExec_t exec;
+    const int rc = nn_graph(e, k, actions, stride, out, &exec);
+    if (rc != CE_OK) return rc;
+    CE_HIP(hipGraphLaunch(exec, e->stream));
+    e->parity ^= (k & 1);
     return CE_OK;
+}
+
+int ce_nn_step_many_prepare(ce_nn_engine *e, int32_t k, const float *actions, int64_t stride,
+                            const ce_multi_outputs *out) {
+    hipGraphExec_t exec;
+    return nn_graph(e, k, actions, stride, out, &exec);
 }
 
 int ce_nn_host_outputs(ce_nn_engine *e, ce_multi_outputs *view) {

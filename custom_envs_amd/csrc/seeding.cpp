@@ -20,6 +20,9 @@
 #include <cstdio>
 #include <cstring>
 
+#include <algorithm>
+#include <vector>
+
 namespace ce {
 namespace {
 
@@ -282,11 +285,17 @@ void reset_draws_nn(uint64_t seed, int n_dims, const int *dims, int n_rows, floa
             for (int i = 0; i < fan_out; ++i) init_weights[off + i] = 0.0f;
         off += fan_out;
     }
-    if (reset_perm) legacy_shuffle(rng, n_rows, reset_perm);
-    if (epoch_perm) {
+    // The kernels stand in for TF's RNG, which is not numpy's: the reset's
+    // shuffle (OptimizeNN.reset -> next() -> on_epoch_end, optimize_nn.py:
+    // 102-120) is the first draw of the fresh env stream, the same
+    // permutation every epoch end inside a step draws.
+    if (reset_perm || epoch_perm) {
         Mt19937 fresh;
         fresh.init_by_array(key, key_len);
-        legacy_shuffle(fresh, n_rows, epoch_perm);
+        std::vector<int32_t> perm(n_rows);
+        legacy_shuffle(fresh, n_rows, perm.data());
+        if (reset_perm) std::copy(perm.begin(), perm.end(), reset_perm);
+        if (epoch_perm) std::copy(perm.begin(), perm.end(), epoch_perm);
     }
 }
 

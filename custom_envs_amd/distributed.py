@@ -13,6 +13,8 @@ under the ``nccl`` backend, gloo in the CPU tests.
 The reference has no multi-GPU code; its scaling unit is one worker per env
 (custom_envs/vectorize/concurrentvecenv.py:74-92).
 """
+from collections.abc import Mapping
+
 import torch
 
 ALIGN = 256
@@ -62,11 +64,55 @@ class PackedLayout:
             out[name] = buf[off:off + size].view(dtype).view((num_envs * rows,) + tail)
         return out
 
+    def rank_views(self, gathered, world):
+        """Zero-copy views of an all-gathered buffer: field -> tensor of shape
+        (world, capacity * rows, *tail), rank r's shard in row r (only its
+        first counts[r] * rows entries are live)."""
+        out = {}
+        for name, dtype, rows, tail in self.fields:
+            size = torch.empty((), dtype=dtype).element_size()
+            flat = gathered.view(dtype)
+            dims = (self.capacity * rows,) + tuple(tail)
+            inner = [1] * len(dims)
+            for i in range(len(dims) - 2, -1, -1):
+                inner[i] = inner[i + 1] * dims[i + 1]
+            out[name] = flat.as_strided((world,) + dims, (self.nbytes // size,) + tuple(inner),
+                                        flat.storage_offset() + self.offsets[name] // size)
+        return out
+
     def unpack(self, gathered, counts):
-        """Global outputs (rank-major) from the all-gathered buffers."""
-        per_rank = gathered.view(len(counts), self.nbytes)
-        parts = [self.views(per_rank[r], c) for r, c in enumerate(counts)]
-        return {name: torch.cat([p[name] for p in parts]) for name, *_ in self.fields}
+        """Global outputs (rank-major = global env order), one copy per field."""
+        views = self.rank_views(gathered, len(counts))
+        rows = {name: r for name, _, r, _ in self.fields}
+        return {name: torch.cat([v[r, :c * rows[name]] for r, c in enumerate(counts)])
+                for name, v in views.items()}
+
+
+class GatheredOutputs(Mapping):
+    """One step's all-gathered outputs.
+
+    ``rank_major[name]`` is a zero-copy (world, capacity * rows, ...) view of
+    the collective's buffer.  ``outputs[name]`` is the global array in env
+    order, built on first access (one copy per field, only for fields a
+    consumer reads)."""
+
+    def __init__(self, layout, gathered, counts):
+        self.layout, self.counts = layout, counts
+        self.rank_major = layout.rank_views(gathered, len(counts))
+        self._rows = {name: r for name, _, r, _ in layout.fields}
+        self._flat = {}
+
+    def __getitem__(self, name):
+        if name not in self._flat:
+            v, rows = self.rank_major[name], self._rows[name]
+            self._flat[name] = torch.cat([v[r, :c * rows] for r, c in enumerate(self.counts)])
+        return self._flat[name]
+
+    def __iter__(self):
+        return iter(self.rank_major)
+
+    def __len__(self):
+        return len(self.rank_major)
 
 
 class ShardedEnvs:
@@ -74,11 +120,18 @@ class ShardedEnvs:
 
     ``engine`` is this rank's engine over ``hi - lo`` envs (``OptimizeEngine``
     or ``MultiOptEngine``); it must expose ``output_fields()``,
-    ``reset_device(out)`` and ``step_device(actions, out)``.
+    ``reset_device(out)`` and ``step_device(actions, out)``.  ``slots`` > 1
+    keeps that many packed output buffers, so the collective of step t can
+    run while step t+1 writes the other buffer (``step(actions, slot)``,
+    ``gather(slot, async_op=True)``).
     """
 
-    def __init__(self, engine, num_envs, rank=0, world=1, group=None, device=None):
+    def __init__(self, engine, num_envs, rank=0, world=1, group=None, device=None, slots=1,
+                 collective=None):
+        """``collective``: run the all-gather even at world 1 (tests the RCCL
+        path on one GPU); default: only when world > 1."""
         self.engine, self.rank, self.world, self.group = engine, rank, world, group
+        self.collective = world > 1 if collective is None else bool(collective)
         self.num_envs = int(num_envs)
         self.lo, self.hi = shard_range(self.num_envs, world, rank)
         if engine.num_envs != self.hi - self.lo:
@@ -88,10 +141,19 @@ class ShardedEnvs:
                                           for r in range(world))]
         self.layout = PackedLayout(engine.output_fields(), max(self.counts))
         device = device if device is not None else torch.device('cuda', torch.cuda.current_device())
-        self.buffer = torch.zeros(self.layout.nbytes, dtype=torch.uint8, device=device)
-        self.out = self.layout.views(self.buffer, engine.num_envs)
-        self.gathered = (torch.empty(world * self.layout.nbytes, dtype=torch.uint8,
-                                     device=device) if world > 1 else None)
+        self.buffers = [torch.zeros(self.layout.nbytes, dtype=torch.uint8, device=device)
+                        for _ in range(slots)]
+        self.outs = [self.layout.views(b, engine.num_envs) for b in self.buffers]
+        self.gathered = [torch.empty(world * self.layout.nbytes, dtype=torch.uint8, device=device)
+                         if self.collective else None for _ in range(slots)]
+
+    @property
+    def buffer(self):
+        return self.buffers[0]
+
+    @property
+    def out(self):
+        return self.outs[0]
 
     @property
     def global_indices(self):
@@ -101,18 +163,23 @@ class ShardedEnvs:
         """Seed = base + global env index: shards reproduce a 1-GPU run."""
         return self.engine.seed([base_seed + g for g in self.global_indices])
 
-    def reset(self):
-        self.engine.reset_device(self.out)
-        return self.out
+    def reset(self, slot=0):
+        self.engine.reset_device(self.outs[slot])
+        return self.outs[slot]
 
-    def step(self, actions):
-        self.engine.step_device(actions, self.out)
-        return self.out
+    def step(self, actions, slot=0):
+        self.engine.step_device(actions, self.outs[slot])
+        return self.outs[slot]
 
-    def gather(self):
-        """Every rank gets the global outputs (rank-major = global env order)."""
-        if self.world == 1:
-            return self.out
+    def gather(self, slot=0, async_op=False):
+        """Every rank gets the global outputs: ONE all_gather_into_tensor of the
+        packed buffer.  Returns ``GatheredOutputs`` (or this rank's outputs at
+        world 1); with ``async_op`` also the collective's work handle, whose
+        ``wait()`` orders the caller's current stream after it."""
+        if not self.collective:
+            return (self.outs[slot], None) if async_op else self.outs[slot]
         import torch.distributed as dist
-        dist.all_gather_into_tensor(self.gathered, self.buffer, group=self.group)
-        return self.layout.unpack(self.gathered, self.counts)
+        work = dist.all_gather_into_tensor(self.gathered[slot], self.buffers[slot],
+                                           group=self.group, async_op=async_op)
+        res = GatheredOutputs(self.layout, self.gathered[slot], self.counts)
+        return (res, work) if async_op else res

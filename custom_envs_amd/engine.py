@@ -192,6 +192,14 @@ class OptimizeEngine:
         check(self._lib.ce_step_many(self._h, int(k), actions.data_ptr(), stride,
                                      ctypes.byref(o)), 'ce_step_many')
 
+    def prepare_many_device(self, k, actions, out, per_step_actions=True):
+        """Instantiate (and upload) the k-step hipGraph without running it."""
+        self._check_device_tensors(actions, out, k if per_step_actions else 1)
+        stride = self.num_envs * self.act_dim if per_step_actions else 0
+        o = self._outputs(out)
+        check(self._lib.ce_step_many_prepare(self._h, int(k), actions.data_ptr(), stride,
+                                             ctypes.byref(o)), 'ce_step_many_prepare')
+
     def wait(self):
         check(self._lib.ce_wait(self._h), 'ce_wait')
 

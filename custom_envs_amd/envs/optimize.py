@@ -7,6 +7,8 @@ custom_envs/envs/baseenvironment.py:11-57.  Same constructor keywords
 ``auto_reset`` off, so stepping past the terminal step behaves like the
 reference (current_step keeps counting, ``done`` stays True).
 """
+import inspect
+
 import numpy as np
 
 from custom_envs_amd.core import Env
@@ -43,6 +45,11 @@ class Optimize(Env):
         """``model='mlp'`` swaps the classifier for the config-3 MLP
         (F -> hidden relu -> K, float32)."""
         from custom_envs_amd.engine import OptimizeEngine
+        # what a VecEnv needs to rebuild this env as one row of a batched engine
+        self.spec_kwargs = self.full_spec(
+            data_set=data_set, batch_size=batch_size, n_of_steps=n_of_steps,
+            max_steps=max_steps, precision=precision, device=device, model=model,
+            hidden=hidden)
         features, targets = resolve_dataset(data_set, batch_size)
         self.engine = OptimizeEngine(features, targets, 1, batch_size=batch_size,
                                      max_steps=max_steps, precision=precision,
@@ -51,6 +58,18 @@ class Optimize(Env):
         self.current_step = 0
         self.observation_space, self.action_space = optimize_spaces(self.engine.act_dim)
         self.seed()
+
+    @staticmethod
+    def full_spec(**kwargs):
+        """Constructor keywords with the defaults filled in (a factory's
+        ``partial(make, 'Optimize-v0', **kw)`` and a built env compare equal)."""
+        params = inspect.signature(Optimize.__init__).parameters
+        spec = {k: p.default for k, p in params.items() if k != 'self'}
+        unknown = set(kwargs) - set(spec)
+        if unknown:
+            raise TypeError('Optimize got unexpected keyword(s) %s' % sorted(unknown))
+        spec.update(kwargs)
+        return spec
 
     def seed(self, seed=None):
         return self.engine.seed([seed])

@@ -164,6 +164,14 @@ class MultiOptEngine:
         stride = self.rows if per_step_actions else 0
         self._call('step_many', int(k), actions.data_ptr(), stride, ctypes.byref(o))
 
+    def prepare_many_device(self, k, actions, out, per_step_actions=True):
+        """Instantiate (and upload) the k-step hipGraph without running it."""
+        if actions.numel() < (k if per_step_actions else 1) * self.rows:
+            raise ValueError('actions tensor too small')
+        o = self._outputs(out)
+        stride = self.rows if per_step_actions else 0
+        self._call('step_many_prepare', int(k), actions.data_ptr(), stride, ctypes.byref(o))
+
     def wait(self):
         self._call('wait')
 

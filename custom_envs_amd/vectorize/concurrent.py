@@ -22,25 +22,81 @@ from custom_envs_amd.spaces import Dict
 ENGINE_IDS = {'Optimize-v0'}
 
 
+def spec_key(kwargs):
+    """Hashable identity of an env spec's keywords: plain values by value,
+    anything else (arrays, data-set objects) by object identity."""
+    def key(v):
+        if v is None or isinstance(v, (str, int, float, bool)):
+            return v
+        if isinstance(v, (list, tuple)) and all(
+                x is None or isinstance(x, (str, int, float, bool)) for x in v):
+            return tuple(v)
+        return ('id', id(v))
+    return tuple(sorted((k, key(v)) for k, v in kwargs.items()))
+
+
+def monitor_parts(fn):
+    """``partial(Monitor, target, path, **kw)`` -> (target, (path, kw)); any
+    other factory -> (fn, None).  The scripts' utils_logging.Monitor
+    (run_multiagent_exp_single.py:78-86, search_optimize_hyperparam.py:
+    99-112); its ``.mon.csv`` rows are what ``VecMonitor`` writes."""
+    from custom_envs_amd.utils.utils_logging import Monitor
+    if not (isinstance(fn, functools.partial) and fn.func is Monitor):
+        return fn, None
+    if not fn.args:
+        return None, None
+    kw = dict(fn.keywords)
+    path = fn.args[1] if len(fn.args) > 1 else kw.pop('file_path', None)
+    kw.pop('allow_early_resets', None)      # run_multiagent_exp_single.py:80
+    return fn.args[0], (path, kw)
+
+
+def monitor_request(monitors):
+    """One VecMonitor setting for a factory list, or False if they disagree."""
+    if all(m is None for m in monitors):
+        return None
+    if any(m is None for m in monitors):
+        return False
+    if len({repr(sorted(m[1].items())) for m in monitors}) != 1:
+        return False
+    return [m[0] for m in monitors], dict(monitors[0][1])
+
+
 def _engine_request(env_fns):
-    """(env_id, kwargs) if all factories build the same engine-backed env."""
-    from custom_envs_amd.core import make
+    """(kwargs, monitor, built) if all factories build the same Optimize-v0
+    spec: ``partial(make | gym.make, 'Optimize-v0', **kw)``,
+    ``partial(Optimize, **kw)``, each optionally inside ``partial(Monitor,
+    ..., path, info_keywords=..., chunk_size=...)`` (also around an env
+    instance, e.g. ``partial(Monitor, gym.make(...), ...)``).  ``built``
+    lists instances the caller created eagerly (the engine replaces them)."""
+    from custom_envs_amd.core import make_request
     from custom_envs_amd.envs.optimize import Optimize
-    first = None
+    keys, specs, monitors, built = [], [], [], []
     for fn in env_fns:
-        if not isinstance(fn, functools.partial):
+        target, monitor = monitor_parts(fn)
+        try:
+            if isinstance(target, Optimize):
+                kwargs = dict(target.spec_kwargs)
+                built.append(target)
+            elif isinstance(target, functools.partial) and target.func is Optimize and \
+                    not target.args:
+                kwargs = Optimize.full_spec(**target.keywords)
+            else:
+                req = make_request(target)
+                if req is None or req[0] not in ENGINE_IDS:
+                    return None
+                kwargs = Optimize.full_spec(**req[1])
+        except TypeError:            # keywords Optimize does not take: not batchable
             return None
-        if fn.func is make and len(fn.args) == 1 and fn.args[0] in ENGINE_IDS:
-            req = (fn.args[0], dict(fn.keywords))
-        elif fn.func is Optimize and not fn.args:
-            req = ('Optimize-v0', dict(fn.keywords))
-        else:
-            return None
-        if first is None:
-            first = req
-        elif req != first:
-            return None
-    return first
+        keys.append(spec_key(kwargs))
+        specs.append(kwargs)
+        monitors.append(monitor)
+    if not specs or len(set(keys)) != 1:
+        return None
+    mon = monitor_request(monitors)
+    if mon is False:
+        return None
+    return specs[0], mon, built
 
 
 class _Cloud:
@@ -107,7 +163,10 @@ class ConcurrentVecEnv:
         self._gpu = None
         if request is not None:
             from custom_envs_amd.vectorize.gpuvecenv import GPUVecEnv
-            self._gpu = GPUVecEnv(len(env_fns), **request[1])
+            kwargs, mon, built = request
+            for env in built:      # single-env engines the caller built eagerly
+                env.close()
+            self._gpu = GPUVecEnv(len(env_fns), monitor=mon, **kwargs)
             self.num_envs = self._gpu.num_envs
             self.observation_space = self._gpu.observation_space
             self.action_space = self._gpu.action_space

@@ -20,13 +20,18 @@ from custom_envs_amd.envs.optimize import optimize_spaces, resolve_dataset
 
 
 class LazyInfos:
-    """Per-env info dicts materialised on access (no O(E) dict build per step)."""
+    """Per-env info dicts materialised on access (no O(E) dict build per step).
 
-    def __init__(self, objective, accuracy, reward, episode_len):
+    ``episodes`` maps env index -> the Monitor's episode record for envs a
+    ``VecMonitor`` closed this step (utils_logging.py:98-116 replaces
+    ``info['episode']`` with it)."""
+
+    def __init__(self, objective, accuracy, reward, episode_len, episodes=None):
         self._objective = objective
         self._accuracy = accuracy
         self._reward = reward
         self._episode_len = episode_len
+        self.episodes = {} if episodes is None else episodes
 
     def __len__(self):
         return len(self._objective)
@@ -37,9 +42,11 @@ class LazyInfos:
         if idx < 0:
             idx += len(self)
         reward = float(self._reward[idx])
+        episode = self.episodes.get(idx)
         return {'objective': float(self._objective[idx]),
                 'accuracy': float(self._accuracy[idx]),
-                'episode': {'r': reward, 'l': int(self._episode_len[idx])}}
+                'episode': {'r': reward, 'l': int(self._episode_len[idx])}
+                if episode is None else episode}
 
     def __iter__(self):
         return (self[i] for i in range(len(self)))
@@ -53,14 +60,25 @@ class GPUVecEnv:
 
     def __init__(self, num_envs, data_set='gaussians_256x10', batch_size=None,
                  n_of_steps=None, max_steps=40, precision=None, device=0, seed=None,
-                 model='linear', hidden=64):
+                 model='linear', hidden=64, monitor=None):
+        """``monitor``: None, or (file paths, Monitor keywords) -- the batched
+        form of wrapping every env in utils_logging.Monitor
+        (utils_logging.py:159-175); writes the same ``.mon.csv`` chunks."""
         from custom_envs_amd.engine import OptimizeEngine
+        from custom_envs_amd.utils.utils_logging import VecMonitor
         features, targets = resolve_dataset(data_set, batch_size)
         self.engine = OptimizeEngine(features, targets, num_envs, batch_size=batch_size,
                                      max_steps=max_steps, precision=precision, device=device,
                                      auto_reset=True, model=model, hidden=hidden)
         self.num_envs = int(num_envs)
         self.observation_space, self.action_space = optimize_spaces(self.engine.act_dim)
+        self.monitor = None
+        if monitor is not None:
+            paths, mkw = monitor
+            self.monitor = VecMonitor(self.num_envs, paths,
+                                      info_keywords=mkw.get('info_keywords', ()),
+                                      chunk_size=mkw.get('chunk_size', 1),
+                                      callbacks=mkw.get('callbacks'))
         self.current_step = np.zeros(self.num_envs, np.int64)
         self.waiting = False
         self.closed = False
@@ -73,8 +91,19 @@ class GPUVecEnv:
             return self.engine.seed(seed)
         return self.engine.seed(list(seed))
 
+    @property
+    def single_observation_space(self):
+        """gym.vector.VectorEnv name of one env's space (SB's observation_space)."""
+        return self.observation_space
+
+    @property
+    def single_action_space(self):
+        return self.action_space
+
     def reset(self):
         self.current_step[:] = 0
+        if self.monitor is not None:
+            self.monitor.reset()
         return self.engine.reset()
 
     def step_async(self, actions):
@@ -89,7 +118,10 @@ class GPUVecEnv:
         self.current_step[:] = np.where(dones, 0, ep_len)
         reward = out['reward'].copy()
         infos = LazyInfos(out['objective'].copy(), out['accuracy'].copy(), reward, ep_len)
-        return out['obs'].copy(), reward, dones, infos
+        obs = out['obs'].copy()
+        if self.monitor is not None:
+            infos.episodes.update(self.monitor.step(reward, dones, infos, obs))
+        return obs, reward, dones, infos
 
     def step(self, actions):
         self.step_async(actions)
@@ -97,6 +129,8 @@ class GPUVecEnv:
 
     def close(self):
         if not self.closed:
+            if self.monitor is not None:
+                self.monitor.close()
             self.engine.close()
             self.closed = True
 
@@ -141,6 +175,10 @@ class GPUVecEnv:
             return [[seeds[i]] for i in idx]
         if method_name in ('render', 'close'):
             return [None] * len(idx)
+        monitor_methods = ('get_episode_rewards', 'get_episode_lengths', 'get_episode_times',
+                           'get_total_steps')
+        if method_name in monitor_methods and self.monitor is not None:
+            return getattr(self.monitor, method_name)(idx)
         raise AttributeError('GPUVecEnv has no per-env method %r' % method_name)
 
     @property
@@ -155,3 +193,49 @@ class GPUVecEnv:
             self.close()
         except Exception:
             pass
+
+
+def batch_space(space, n):
+    """gym.vector.utils.batch_space for a Box: the stacked (n, ...) space."""
+    from custom_envs_amd.spaces import Box
+    return Box(low=np.broadcast_to(space.low, (n,) + space.shape),
+               high=np.broadcast_to(space.high, (n,) + space.shape),
+               shape=(n,) + space.shape, dtype=space.dtype)
+
+
+class VectorEnv(GPUVecEnv):
+    """The same engine behind the ``gym.vector.VectorEnv`` surface the north
+    star names: ``observation_space``/``action_space`` are the batched
+    spaces, ``single_observation_space``/``single_action_space`` one env's
+    (GPUVecEnv keeps stable-baselines' convention, where the plain names are
+    one env's spaces).  ``reset() -> obs``, ``step(actions) -> (obs, rewards,
+    dones, infos)`` with auto-reset, as gym<=0.21's vector envs."""
+    is_vector_env = True
+
+    def __init__(self, num_envs, **kwargs):
+        super().__init__(num_envs, **kwargs)
+        self._single = (self.observation_space, self.action_space)
+        self.observation_space = batch_space(self._single[0], self.num_envs)
+        self.action_space = batch_space(self._single[1], self.num_envs)
+
+    @property
+    def single_observation_space(self):
+        return self._single[0]
+
+    @property
+    def single_action_space(self):
+        return self._single[1]
+
+    def get_attr(self, attr_name, indices=None):
+        if attr_name in ('observation_space', 'action_space'):
+            space = self._single[0 if attr_name == 'observation_space' else 1]
+            return [space] * len(self._indices(indices))
+        return super().get_attr(attr_name, indices)
+
+
+def make_vec(env_id, num_envs, **kwargs):
+    """``gym.vector.make(id, num_envs, **kw)`` for the engine-backed ids: ONE
+    engine for all envs instead of num_envs worker processes."""
+    if env_id != 'Optimize-v0':
+        raise KeyError('make_vec serves Optimize-v0; MultiOptLRs-v0 batches through OptVecEnv')
+    return VectorEnv(num_envs, **kwargs)

@@ -57,53 +57,42 @@ class OptEnvRunner:
 
 
 def _env_spec(obj):
-    """MultiOptLRs kwargs an object or factory stands for, else None."""
-    from custom_envs_amd.core import make
+    """MultiOptLRs kwargs an object or factory stands for, else None:
+    an instance, ``partial(MultiOptLRs, **kw)`` or ``partial(make | gym.make,
+    'MultiOptLRs-v0', **kw)`` (search_optimize_hyperparam.py:100-103)."""
+    from custom_envs_amd.core import make_request
     from custom_envs_amd.envs.multioptlrs import MultiOptLRs
     if isinstance(obj, MultiOptLRs):
         return dict(obj.spec_kwargs), obj
-    if isinstance(obj, functools.partial):
-        if obj.func is make and obj.args == ('MultiOptLRs-v0',):
-            return dict(obj.keywords), None
-        if obj.func is MultiOptLRs and not obj.args:
-            return dict(obj.keywords), None
+    if isinstance(obj, functools.partial) and obj.func is MultiOptLRs and not obj.args:
+        return dict(obj.keywords), None
+    req = make_request(obj)
+    if req is not None and req[0] == 'MultiOptLRs-v0':
+        return req[1], None
     return None
 
 
 def _batch_request(environment_fns):
     """(env kwargs, monitor settings or None, built envs to close) or None."""
-    from custom_envs_amd.utils.utils_logging import Monitor
-    specs, monitors, built = [], [], []
+    from custom_envs_amd.vectorize.concurrent import monitor_parts, monitor_request, spec_key
+    keys, specs, monitors, built = [], [], [], []
     for fn in environment_fns:
-        monitor = None
-        target = fn
-        if isinstance(fn, functools.partial) and fn.func is Monitor:
-            if not fn.args:
-                return None
-            target = fn.args[0]
-            kw = dict(fn.keywords)
-            path = fn.args[1] if len(fn.args) > 1 else kw.pop('file_path', None)
-            kw.pop('allow_early_resets', None)   # run_multiagent_exp_single.py:80
-            monitor = (path, kw)
+        target, monitor = monitor_parts(fn)
         spec = _env_spec(target)
         if spec is None:
             return None
         kwargs, instance = spec
-        specs.append(tuple(sorted((k, tuple(v) if isinstance(v, list) else v)
-                                  for k, v in kwargs.items())))
+        keys.append(spec_key(kwargs))
+        specs.append(kwargs)
         monitors.append(monitor)
         if instance is not None:
             built.append(instance)
-    if len(set(specs)) != 1:
+    if not specs or len(set(keys)) != 1:
         return None
-    if any(m is None for m in monitors) and any(m is not None for m in monitors):
+    mon = monitor_request(monitors)
+    if mon is False:
         return None
-    mon = None
-    if monitors[0] is not None:
-        if len({repr(sorted(m[1].items())) for m in monitors}) != 1:
-            return None
-        mon = ([m[0] for m in monitors], dict(monitors[0][1]))
-    return dict(specs[0]), mon, built
+    return specs[0], mon, built
 
 
 class _RowInfos:
@@ -261,9 +250,22 @@ class OptVecEnv:
                            'get_total_steps')
         if method_name in monitor_methods and self.monitor is not None:
             return getattr(self.monitor, method_name)(indices)
-        if method_name in ('render', 'seed'):
-            E = self._engine.num_envs
-            return [None] * (E if indices is None else len(indices))
+        E = self._engine.num_envs
+        idx = list(range(E)) if indices is None else (
+            [indices] if isinstance(indices, int) else list(indices))
+        if method_name == 'seed':
+            # BaseEnvironment.seed per env (baseenvironment.py:20-28); the
+            # 'nn' problem draws its weights and shuffles from these seeds
+            from custom_envs_amd.engine import normalize_seed
+            seed = method_args[0] if method_args else method_kwargs.get('seed')
+            seeds = list(getattr(self, '_seeds', range(E)))
+            for i in idx:
+                seeds[i] = normalize_seed(seed)
+            self._engine.seed(seeds)
+            self._seeds = seeds
+            return [[seeds[i]] for i in idx]
+        if method_name == 'render':
+            return [None] * len(idx)
         raise AttributeError('engine-backed OptVecEnv has no per-env method %r' % method_name)
 
     def render(self, *args, **kwargs):

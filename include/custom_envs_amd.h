@@ -23,6 +23,10 @@
  *   ce_wait        ConcurrentVecEnv.step_wait    custom_envs/vectorize/concurrentvecenv.py:102-107
  *   ce_step_many   K consecutive VecEnv.step calls with device-resident actions
  *                  (benchmark / GPU-resident agent mode; one hipGraph)
+ *   ce_step_many_prepare
+ *                  instantiate + upload that hipGraph without running it (graphs
+ *                  are cached per (k, actions, stride, outputs, stream), so a
+ *                  timed region never captures)
  *   ce_get_state / ce_set_state
  *                  the per-env attributes model.weights, loss_hist, grad_hist,
  *                  current_step (optimize.py:45-50, baseenvironment.py:18)
@@ -37,7 +41,7 @@
  *   ce_multi_step    OptVecEnv.step_async/wait    custom_envs/vectorize/optvecenv.py:70-88
  *                    -> OptEnvRunner.step         custom_envs/vectorize/optvecenv.py:38-46
  *                    -> MultiOptLRs.base_step     custom_envs/envs/multioptlrs.py:80-129
- *   ce_multi_step_async / ce_multi_wait / ce_multi_step_many / ce_multi_host_outputs /
+ *   ce_multi_step_async / ce_multi_wait / ce_multi_step_many(_prepare) / ce_multi_host_outputs /
  *   ce_multi_get_state / ce_multi_set_stream / ce_multi_destroy: as for Optimize-v0.
  *
  * MultiOptLRs-v0 over the neural-network problem (get_problem('nn')):
@@ -51,7 +55,7 @@
  *   ce_nn_reset      OptVecEnv.reset -> MultiOptLRs.base_reset  multioptlrs.py:66-78
  *   ce_nn_step       OptVecEnv.step -> MultiOptLRs.base_step    multioptlrs.py:80-129
  *                    (+ OptimizeNN.get_gradient/get/next, optimize_nn.py:102-159)
- *   ce_nn_step_async / ce_nn_wait / ce_nn_step_many / ce_nn_host_outputs /
+ *   ce_nn_step_async / ce_nn_wait / ce_nn_step_many(_prepare) / ce_nn_host_outputs /
  *   ce_nn_get_state / ce_nn_set_stream / ce_nn_destroy / ce_nn_n_params:
  *                    as for ce_multi_*.
  *
@@ -176,6 +180,8 @@ int ce_wait(ce_engine *eng);
 int ce_step_many(ce_engine *eng, int32_t k, const float *actions,
                  int64_t action_step_stride /* elements between steps */,
                  const ce_outputs *out /* device pointers */);
+int ce_step_many_prepare(ce_engine *eng, int32_t k, const float *actions,
+                         int64_t action_step_stride, const ce_outputs *out);
 
 /* Pinned host buffers holding the last host-mode outputs (zero-copy views). */
 int ce_host_outputs(ce_engine *eng, ce_outputs *view);
@@ -242,6 +248,8 @@ int ce_multi_step_async(ce_multi_engine *eng, const float *actions,
 int ce_multi_wait(ce_multi_engine *eng);
 int ce_multi_step_many(ce_multi_engine *eng, int32_t k, const float *actions,
                        int64_t action_step_stride, const ce_multi_outputs *out);
+int ce_multi_step_many_prepare(ce_multi_engine *eng, int32_t k, const float *actions,
+                               int64_t action_step_stride, const ce_multi_outputs *out);
 int ce_multi_host_outputs(ce_multi_engine *eng, ce_multi_outputs *view);
 /* theta [E][P] (problem parameters in agent order) and current_step [E] */
 int ce_multi_get_state(ce_multi_engine *eng, float *theta, int32_t *step);
@@ -294,6 +302,8 @@ int ce_nn_step_async(ce_nn_engine *eng, const float *actions, const ce_multi_out
 int ce_nn_wait(ce_nn_engine *eng);
 int ce_nn_step_many(ce_nn_engine *eng, int32_t k, const float *actions,
                     int64_t action_step_stride, const ce_multi_outputs *out);
+int ce_nn_step_many_prepare(ce_nn_engine *eng, int32_t k, const float *actions,
+                            int64_t action_step_stride, const ce_multi_outputs *out);
 int ce_nn_host_outputs(ce_nn_engine *eng, ce_multi_outputs *view);
 /* theta [E][P] (agent order), gprev [E][P] (newest raw-history gradient),
    step [E], cursor [E] (batch index in the epoch), order [E][N] (dataset row

@@ -27,19 +27,22 @@ MultiOptLRs env drives it (custom_envs/envs/multioptlrs.py:39-129):
 TensorFlow is absent from this image, so two pieces are build-defined and
 the float32 values are "parity unpinned" against TF itself:
   * initialisation: Keras draws glorot-uniform kernels from TF's RNG (not
-    reproducible); here each kernel is ``npr.uniform(-l, l)`` with
-    l = sqrt(6 / (fan_in + fan_out)) from the env's RandomState (the global
-    npr inside use_random_state), kernels in layer order, zero biases,
-    rounded to float32 -- the same rule as the config-3 MLP
-    (oracle/optimize.py ModelMLP);
+    reproducible, and separate from numpy's); here each kernel is
+    ``uniform(-l, l)`` with l = sqrt(6 / (fan_in + fan_out)), kernels in
+    layer order, zero biases, rounded to float32 -- the same rule as the
+    config-3 MLP (oracle/optimize.py ModelMLP) -- drawn from a stand-in for
+    TF's RNG: a RandomState started at the env RNG's seeded state.  Like
+    TF's, it does not advance the global npr, so the reset's shuffle
+    (next() -> on_epoch_end, optimize_nn.py:102-120) is the first draw of
+    the fresh env stream, the same permutation as every epoch end;
   * the loss: tf.keras (>= 1.13) routes categorical_crossentropy of a
     Softmax output through softmax_cross_entropy_with_logits on the logits:
     CE_i = log(sum_k exp(z_ik - m_i)) - (z_iy - m_i), dCE/dz = softmax - y.
 Because use_random_state hands the step a fresh copy of the env RNG, every
 epoch-end reshuffle inside a step draws the same permutation (the first
-legacy shuffle of arange(N) from the seed), and every reset draws the kernels
-then one shuffle from the same start: both are fixed per seed, and the row
-order composes them episode after episode.
+legacy shuffle of arange(N) from the seed), and so does every reset: the
+permutation is fixed per seed, and the row order composes it at every reset
+and every epoch end.
 """
 import numpy as np
 import numpy.random as npr
@@ -74,11 +77,14 @@ class OptimizeNN:
 
     # --- BaseProblem surface used by MultiOptLRs ------------------------------
     def reset(self):
-        """:114-120 under the env's use_random_state (build-defined init)."""
+        """:114-120 under the env's use_random_state (build-defined init from
+        the TF-RNG stand-in; the global npr is not advanced)."""
+        tf_rng = np.random.RandomState()
+        tf_rng.set_state(npr.get_state())
         parts = []
         for a, b in zip(self.dims[:-1], self.dims[1:]):
             limit = np.sqrt(6.0 / (a + b))
-            parts.append(npr.uniform(-limit, limit, (a, b)).ravel())
+            parts.append(tf_rng.uniform(-limit, limit, (a, b)).ravel())
             parts.append(np.zeros(b))
         self.params = np.concatenate(parts).astype(np.float32)
         self.data_set_iter = iter(())
@@ -182,14 +188,16 @@ class MultiOptLRsNN(MultiOptLRs):
 
 def nn_draws(seed, dims, n_rows):
     """(theta0, reset_perm, epoch_perm) of an env seeded with ``seed``: the
-    kernels then one shuffle at every reset, and the shuffle every epoch end
-    inside a step draws (both from the never-advanced env RandomState)."""
+    kernels (TF-RNG stand-in), the shuffle of every reset and the shuffle of
+    every epoch end inside a step.  The two shuffles are both the first draw
+    of the never-advanced env RandomState, so they are equal."""
     rng, _ = np_random(seed)
     parts = []
     for a, b in zip(dims[:-1], dims[1:]):
         limit = np.sqrt(6.0 / (a + b))
         parts.append(rng.uniform(-limit, limit, (a, b)).ravel())
         parts.append(np.zeros(b))
+    rng, _ = np_random(seed)
     reset_perm = np.arange(n_rows)
     rng.shuffle(reset_perm)
     rng, _ = np_random(seed)

@@ -41,12 +41,13 @@ def _dataset(n_features, n_rows=200, seed=3):
     return x, np.eye(2)[y]
 
 
-def _rollout(dataset, pair_u, num_envs, batch_size, steps=43):
+def _rollout(dataset, pair_u, num_envs, batch_size, steps=43, precision='f64'):
     from custom_envs_amd.engine import OptimizeEngine
     saved = {k: os.environ.get(k) for k in ('CE_PAIR_U',)}
     os.environ['CE_PAIR_U'] = str(pair_u)
     try:
-        eng = OptimizeEngine(*dataset, num_envs=num_envs, batch_size=batch_size)
+        eng = OptimizeEngine(*dataset, num_envs=num_envs, batch_size=batch_size,
+                             precision=precision)
     finally:
         for k, v in saved.items():
             if v is None:
@@ -63,7 +64,21 @@ def _rollout(dataset, pair_u, num_envs, batch_size, steps=43):
     return seeds, acts, outs
 
 
-def _check_against_oracle(dataset, batch_size, seeds, acts, outs, envs):
+def _close_f32_row(got, ref, tol=1e-5, elem_tol=1e-3, elem_floor=1e-2):
+    """f32 engine: ||d||_inf / ||ref||_inf <= 1e-5 per obs row (the north-star
+    bound) and 1e-3 elementwise where |ref| >= 1e-2 ||ref||_inf (as
+    test_gpu_parity.py)."""
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    scale = max(np.abs(ref).max(), 1e-30)
+    assert np.abs(got - ref).max() / scale <= tol
+    big = np.abs(ref) >= elem_floor * scale
+    assert np.all(np.abs(got - ref)[big] <= elem_tol * np.abs(ref)[big])
+
+
+def _check_against_oracle(dataset, batch_size, seeds, acts, outs, envs, precision='f64'):
+    if precision == 'f32':
+        _check_f32(dataset, batch_size, seeds, acts, outs, envs)
+        return
     for i in envs:
         env = OracleEnv(*dataset, batch_size=batch_size)
         env.seed(seeds[i])
@@ -111,3 +126,70 @@ def test_pair_and_wave_kernels_agree_closely():
         np.testing.assert_allclose(oa['obs'], ob['obs'], rtol=2e-6, atol=1e-9)
         assert np.array_equal(oa['done'], ob['done'])
         assert np.array_equal(oa['accuracy'], ob['accuracy'])
+
+
+def _check_f32(dataset, batch_size, seeds, acts, outs, envs):
+    n_rows = len(dataset[0])
+    for i in envs:
+        env = OracleEnv(*dataset, batch_size=batch_size)
+        env.seed(seeds[i])
+        env.reset()
+        for t in range(acts.shape[0]):
+            obs, rew, done, info = env.step(acts[t, i])
+            if done:
+                obs = env.reset()
+            out = outs[t]
+            assert bool(out['done'][i]) == done, (i, t)
+            assert out['episode_len'][i] == info['episode']['l']
+            if not done:
+                _close_f32_row(out['obs'][i], obs)
+            else:
+                assert np.all(out['obs'][i] == 0)
+            assert out['reward'][i] == pytest.approx(rew, rel=1e-5)
+            assert out['objective'][i] == pytest.approx(info['objective'], rel=1e-5)
+            # a float32 logit near a tie may flip one row's argmax
+            assert abs(out['accuracy'][i] - info['accuracy']) <= 1.5 / n_rows
+
+
+@pytest.mark.parametrize('pair_u', [0, 1])
+@pytest.mark.parametrize('batch_size', [None, 32])
+def test_f32_paths_odd_env_count(pair_u, batch_size):
+    """The f32 engine (U = 1 pair kernel by default, and one env per wave) at
+    an odd env count: the last wave's second half has no env."""
+    ds = _dataset(10)
+    E = 37
+    seeds, acts, outs = _rollout(ds, pair_u, E, batch_size, precision='f32')
+    _check_against_oracle(ds, batch_size, seeds, acts, outs, [0, 1, 18, 35, 36],
+                          precision='f32')
+
+
+def _multiclass(n_features, n_classes, n_rows=150, seed=5):
+    """(features, one-hot targets) with K > 2 classes; (4, 3) is the
+    iris-shaped set of load_data's default (the reference's iris.npz is a
+    git-LFS pointer), the rest are make_classification sets."""
+    if (n_features, n_classes) == (4, 3):
+        from custom_envs_amd.data import load_data
+        seq = load_data('iris_synthetic', batch_size=None)
+        return seq.features, seq.targets
+    if n_features < 5:
+        rs = np.random.RandomState(seed)
+        centers = rs.normal(0, 2, (n_classes, n_features))
+        y = np.arange(n_rows) % n_classes
+        x = centers[y] + rs.normal(0, 1, (n_rows, n_features))
+        return x, np.eye(n_classes)[y]
+    from sklearn.datasets import make_classification
+    x, y = make_classification(n_samples=n_rows, n_features=n_features, n_informative=4,
+                               n_classes=n_classes, random_state=seed)
+    return x, np.eye(n_classes)[y]
+
+
+@pytest.mark.parametrize('precision', ['f64', 'f32'])
+@pytest.mark.parametrize('batch_size', [None, 32])
+@pytest.mark.parametrize('shape', [(4, 3), (10, 3), (10, 4), (3, 3)])
+def test_general_k_softmax(shape, batch_size, precision):
+    """The literal softmax classifier (SoftmaxModel, K > 2) at every compiled
+    K > 2 shape: full batch and B = 32, across an auto-reset, both engines."""
+    ds = _multiclass(*shape)
+    E = 21
+    seeds, acts, outs = _rollout(ds, 0, E, batch_size, precision=precision)
+    _check_against_oracle(ds, batch_size, seeds, acts, outs, [0, 10, 20], precision=precision)
