@@ -7,14 +7,16 @@ pointer or a missing file raises ``RuntimeError``.
   load_mnist / load_emnist   IDX-ubyte label + image files, .xz (the
                              reference's), .gz or raw (load_data.py:15-44)
   resize_nearest             PIL ``Image.resize(shape, NEAREST)`` for uint8
-                             images (utils_image.py:6-25): output pixel x
-                             samples source floor((x + 0.5) * in / out)
+                             images (utils_image.py:6-25)
   iris / skin                the .npz 'data' array / tab-separated text with
                              the label in the last column (load_data.py:61-64,
                              79-83)
-PIL is absent from this image, so the resize is "parity unpinned" against
-PIL itself; tests pin it against torch's 'nearest-exact' interpolation, which
-uses the same pixel-centre rule.
+The resize restates Pillow's scale-only affine path (ImagingScaleAffine):
+source index = int(o) with o starting at s/2 and advanced by s = in/out in
+float64 per output pixel -- an accumulated sum, which is not always
+floor((x + 0.5) s).  tests/test_ref_pins.py pins it bit for bit against the
+reference's own utils_image.resize_array_many (numpy + PIL, both importable
+in the build container; fixture tests/golden/ref_load_data.npz).
 """
 import gzip
 import lzma
@@ -75,14 +77,25 @@ def load_emnist(data_dir, name='emnist', kind='train'):
     return images.reshape(len(labels), -1), labels
 
 
+def _nearest_positions(n_in, n_out):
+    """Source index of each output pixel, in Pillow's float64 accumulation order."""
+    scale = n_in / n_out
+    pos = np.empty(n_out, np.int64)
+    o = scale * 0.5
+    for i in range(n_out):
+        pos[i] = int(o)
+        o += scale
+    return pos
+
+
 def resize_nearest(images, shape):
     """PIL NEAREST resize of uint8 images [n][h][w] to shape = (width, height)
     (PIL's order, utils_image.py:14)."""
     images = np.asarray(images)
     h, w = images.shape[-2:]
     out_w, out_h = shape
-    ys = np.floor((np.arange(out_h) + 0.5) * (h / out_h)).astype(np.int64)
-    xs = np.floor((np.arange(out_w) + 0.5) * (w / out_w)).astype(np.int64)
+    ys = _nearest_positions(h, out_h)
+    xs = _nearest_positions(w, out_w)
     return images[..., ys[:, None], xs[None, :]]
 
 

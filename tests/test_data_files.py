@@ -1,10 +1,9 @@
 """File-backed data sets (custom_envs/data/load_data.py:15-104) on files the
 test writes itself: IDX-ubyte (.xz, as the reference ships them, and .gz),
 the iris .npz and the skin text table.  The reference's own files are
-git-LFS pointers; the loader refuses them.  PIL is absent, so the NEAREST
-resize is pinned against torch's 'nearest-exact' (same pixel-centre rule)
-and against the explicit source-pixel indices 2, 6, ..., 26 of a 28 -> 7
-PIL NEAREST resize."""
+git-LFS pointers; the loader refuses them.  The NEAREST resize is pinned
+against PIL itself here (Pillow is importable in this image) and against the
+reference's utils_image in tests/test_ref_pins.py."""
 import gzip
 import lzma
 import os
@@ -50,15 +49,15 @@ def test_idx_sets(tmp_path, compress, name, sub, prefix):
     assert len(ds) == 5 and ds.feature_shape == (49,)
 
 
-def test_resize_matches_nearest_exact():
-    import torch
+def test_resize_matches_pil_nearest():
+    from PIL import Image
     rs = np.random.RandomState(1)
-    for (h, w), (ow, oh) in (((28, 28), (7, 7)), ((32, 32), (7, 7)), ((10, 14), (4, 6))):
+    for (h, w), (ow, oh) in (((28, 28), (7, 7)), ((32, 32), (7, 7)), ((10, 14), (4, 6)),
+                             ((28, 28), (9, 5)), ((13, 17), (40, 3))):
         img = rs.randint(0, 256, (3, h, w)).astype(np.uint8)
-        ref = torch.nn.functional.interpolate(torch.from_numpy(img[:, None].astype(np.float32)),
-                                              size=(oh, ow), mode='nearest-exact')
-        np.testing.assert_array_equal(resize_nearest(img, (ow, oh)),
-                                      ref[:, 0].numpy().astype(np.uint8))
+        ref = np.stack([np.asarray(Image.fromarray(im).resize((ow, oh), Image.NEAREST))
+                        for im in img])
+        np.testing.assert_array_equal(resize_nearest(img, (ow, oh)), ref)
 
 
 def test_iris_and_skin_tables(tmp_path):

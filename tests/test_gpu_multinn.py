@@ -123,13 +123,12 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
         if g_prev is not None:
             g_new = _obs_form(_ratio(g_e, g_prev))
             assert np.array_equal(obs[:, 2 * H], g_new), t
-            assert float(step['info'][i, 12]) == pytest.approx(
-                np.mean(np.abs(_ratio(g_e, g_prev))), rel=1e-5)
-            assert float(step['info'][i, 13]) == pytest.approx(
-                np.mean(np.abs(g_e.astype(np.float64) - g_prev)), rel=1e-5, abs=1e-12)
+            _close_f32_info(step['info'][i, 12], np.mean(np.abs(_ratio(g_e, g_prev))), 1e-5)
+            _close_f32_info(step['info'][i, 13], np.mean(np.abs(g_e.astype(np.float64) - g_prev)),
+                            1e-5, 1e-12)
         if l_prev is not None:
             adj_l = float(_ratio(loss, l_prev))
-            assert float(step['info'][i, 11]) == pytest.approx(adj_l, rel=1e-6)
+            _close_f32_info(step['info'][i, 11], adj_l, 1e-6)
             assert np.all(obs[:, H] == _obs_form(adj_l))
         for k, old in enumerate(reversed(ring[-(H - 1):]), start=1):
             assert np.array_equal(obs[:, k], old[:, 0]), (t, k)
@@ -151,6 +150,16 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
 
 def _actions(T, E, P, lo, hi, seed):
     return np.random.RandomState(seed).uniform(lo, hi, (T, E * P)).astype(np.float32)
+
+
+def _close_f32_info(got, expected, rel, abs_tol=None):
+    """Info values are float32 outputs: a float64 mean beyond the float32
+    range (a near-zero previous gradient entry makes |g / g_prev| huge)
+    comes out as +-inf."""
+    if not np.isfinite(np.float32(expected)):
+        assert np.float32(got) == np.float32(expected)
+    else:
+        assert float(got) == pytest.approx(expected, rel=rel, abs=abs_tol)
 
 
 @pytest.mark.parametrize('hidden', [(64,), (96, 32), (32, 64, 128)])
