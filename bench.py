@@ -121,7 +121,8 @@ def parse(argv=None):
     p.add_argument('--warmup', type=int, default=200)
     p.add_argument('--envs', type=int, default=None,
                    help='envs per GPU (default 4096 optimize, 1024 multi)')
-    p.add_argument('--workload', default='optimize', choices=['optimize', 'multi', 'mlp', 'nn'])
+    p.add_argument('--workload', default='optimize',
+                   choices=['optimize', 'multi', 'mlp', 'nn', 'mnist'])
     p.add_argument('--precision', default='f64', choices=['f64', 'f32'])
     p.add_argument('--graph-steps', type=int, default=250, help='steps per hipGraph replay')
     p.add_argument('--no-gather', action='store_true',
@@ -138,6 +139,8 @@ def parse(argv=None):
     p.add_argument('--profile-only', action='store_true',
                    help='run the timed steps only (for rocprofv3)')
     args = p.parse_args(argv)
+    if args.workload == 'mnist' and '--steps' not in (argv or sys.argv):
+        args.steps, args.warmup = 30, 3      # ~13 ms per step at 4096 envs
     if args.envs is None:
         args.envs = {'multi': 1024, 'nn': 1024}.get(args.workload, 4096)
     return args
@@ -305,6 +308,44 @@ def mlp_dataset():
     return seq.features, seq.targets
 
 
+def mnist_dataset():
+    from custom_envs_amd.data import load_data
+    seq = load_data('mnist7x7_synthetic', batch_size=None)
+    return seq.features, seq.targets
+
+
+def build_mnist(args, torch, device, rank, world):
+    """Optimize-v0 at the reference's default data shape (load_data('mnist'):
+    60,000 rows, 7x7 = 49 features, 10 classes; batch_size=None = all rows,
+    optimize.py:40), float64 on the MFMA kernel."""
+    from custom_envs_amd.engine import OptimizeEngine
+    features, targets = mnist_dataset()
+    E = args.envs
+    eng = OptimizeEngine(features, targets, num_envs=E, device=device)
+    eng.seed([rank * E + i for i in range(E)])
+    gen = torch.Generator(device='cuda').manual_seed(99 + rank)
+    S = max(1, min(args.graph_steps, args.steps, 4))
+    actions = torch.randn((S, E, eng.act_dim), generator=gen, device='cuda') * 0.01
+    return eng, actions, S
+
+
+def cpu_baseline_mnist(budget_s):
+    """The reference's path restated (oracle Optimize envs, float64 numpy,
+    under the restated SubprocVecEnv) on the same 60,000 x 49 x 10 set."""
+    from oracle.vectorize import SubprocVecEnv
+    features, targets = mnist_dataset()
+    p = cpu_share()
+    venv = SubprocVecEnv([_optimize_factory(features, targets, i) for i in range(p)], 'fork')
+    venv.reset()
+    acts = np.random.RandomState(0).normal(0, 0.01, (p, 490)).astype(np.float32)
+    steps, wall, _ = _time_cpu(venv, acts, budget_s)
+    venv.close()
+    return {'value': p * steps / wall, 'unit': 'env-steps/s', 'cores': p, 'kind': 'port',
+            'sample': 'SubprocVecEnv %d processes x %d steps (%.1f s wall) of the float64 '
+                      'numpy oracle Optimize env on the 60000 x 49 x 10 set, B = N'
+                      % (p, steps, wall)}
+
+
 def build_mlp(args, torch, device, rank, world, phases=None):
     from custom_envs_amd.engine import OptimizeEngine
     features, targets = mlp_dataset()
@@ -413,7 +454,9 @@ def run_cpu_baseline_child(args):
 
 
 def cpu_baseline_only(args):
-    if args.workload == 'nn':
+    if args.workload == 'mnist':
+        cpu = cpu_baseline_mnist(args.cpu_seconds)
+    elif args.workload == 'nn':
         cpu = cpu_baseline_nn(args.cpu_seconds)
     elif args.workload == 'multi':
         cpu = cpu_baseline_multi(args.envs, args.cpu_seconds)
@@ -507,8 +550,9 @@ def main():
     multi = args.workload == 'multi'
     mlp = args.workload == 'mlp'
     nn = args.workload == 'nn'
+    mnist = args.workload == 'mnist'
     builder = {'optimize': build_optimize, 'multi': build_multi, 'mlp': build_mlp,
-               'nn': build_nn}[args.workload]
+               'nn': build_nn, 'mnist': build_mnist}[args.workload]
     eng, actions, S = builder(args, torch, device, rank, world)
     E = args.envs
     stream = torch.cuda.Stream()          # a real stream: graphs cannot capture the null stream
@@ -572,12 +616,51 @@ def main():
         return 0
 
     modes = {}
+    gather_graph = None
     if gather_modes:
-        primary = run_gather_pipelined
-        run_gather_pipelined(args.warmup)
-        modes['pipelined'] = _timed(torch, dist, run_gather_pipelined, args.steps)
-        run_gather_serial(args.warmup)
-        modes['serial'] = _timed(torch, dist, run_gather_serial, args.steps)
+        # both gather modes also as hipGraphs (torch.cuda.graph capturing the
+        # engine's launches and RCCL's collectives, one replay per chunk):
+        # eager, each step costs a ctypes launch plus a torch collective call
+        # on the host, which is more than the kernel
+        gg_chunk = max(1, min(args.graph_steps, 50))
+
+        def gchunks(k):
+            return [gg_chunk] * (k // gg_chunk) + ([k % gg_chunk] if k % gg_chunk else [])
+
+        run_gather_pipelined(max(args.warmup, 4))     # communicators up before capture
+        run_gather_serial(2)
+        torch.cuda.synchronize()
+        graphs = {}
+        try:
+            for kind, fn in (('pipelined', run_gather_pipelined), ('serial', run_gather_serial)):
+                for n in sorted(set(gchunks(args.warmup) + gchunks(args.steps))):
+                    g = torch.cuda.CUDAGraph()
+                    counter[0] = 0
+                    with torch.cuda.graph(g, stream=stream):
+                        fn(n)
+                    graphs[kind, n] = g
+            torch.cuda.synchronize()
+            gather_graph = True
+        except Exception as exc:          # fall back to eager replays, say so
+            gather_graph = 'eager (capture failed: %s)' % str(exc)[:200]
+            graphs = {}
+            torch.cuda.synchronize()
+
+        def replayer(kind, eager):
+            if not graphs:
+                return eager
+
+            def run(k):
+                for n in gchunks(k):
+                    graphs[kind, n].replay()
+            return run
+
+        run_pipe = replayer('pipelined', run_gather_pipelined)
+        run_ser = replayer('serial', run_gather_serial)
+        run_pipe(args.warmup)
+        modes['pipelined'] = _timed(torch, dist, run_pipe, args.steps)
+        run_ser(args.warmup)
+        modes['serial'] = _timed(torch, dist, run_ser, args.steps)
         run_graph(args.warmup)
         modes['no_gather'] = _timed(torch, dist, run_graph, args.steps)
         elapsed = modes['pipelined']
@@ -635,6 +718,8 @@ def main():
                             phase_ms)
         elif nn:
             line = nn_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard)
+        elif mnist:
+            line = mnist_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean)
         else:
             line = (multi_line if multi else optimize_line)(args, eng, world, E, S, elapsed,
                                                             kernel_ms, kernel_ms_mean, shard)
@@ -644,6 +729,7 @@ def main():
             line['value_no_gather'] = units / modes['no_gather']
             line['ms_per_step_modes'] = {k: v / args.steps * 1e3 for k, v in modes.items()}
             line['gather_bytes_per_rank'] = shard.layout.nbytes
+            line['gather_graph'] = gather_graph
         line['cpu_baseline'] = cpu
         if host_rate is not None:
             line['host_loop_env_steps_per_s'] = host_rate
@@ -804,6 +890,39 @@ def nn_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
             'mfma_tflops': flops * E / (kernel_ms * 1e-3) / 1e12,
             'mfma_peak_tflops': MFMA_F32_PEAK_TFLOPS,
         },
+    })
+    return line
+
+
+METRIC_MNIST = ('vectorised env-steps/sec, Optimize-v0 at the reference default data shape '
+                '(mnist 7x7: 60000 x 49, 10 classes, B = N) @4096 envs, MI355X vs host CPU')
+MFMA_F64_PEAK_TFLOPS = 78.6    # MI355X spec, f64 matrix (measured 71: profiles/r02_mfma_f64.jsonl)
+
+
+def mnist_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean):
+    N, F, K = eng.n_rows, eng.n_features, eng.n_classes
+    flops = 4 * N * F * K            # X W (2NFK) and X^T (P - Y) (2NFK) per env-step
+    achieved = flops * E / (kernel_ms * 1e-3) / 1e12
+    line = {'metric': METRIC_MNIST}
+    line.update(_common(args, world, E, S, elapsed, None))
+    line.update({
+        'dtype': 'f64',
+        'data': 'synthetic mnist7x7_synthetic: 60000 28x28 uint8 blob digits sampled at the '
+                'PIL NEAREST 28->7 pixels, normalised, 10 classes; actions N(0, 0.01) float32 '
+                'generated on device',
+        'config': {'workload': 'Optimize-v0 softmax regression 49 x 10 (P=490, obs 981) over '
+                               'N=60000 rows, B=N, %d envs per GPU, in-kernel auto-reset, '
+                               'device-resident actions/outputs' % E,
+                   'envs_per_gpu': E, 'global_envs': world * E, 'n_rows': N, 'n_features': F,
+                   'n_classes': K, 'batch_size': eng.batch_size,
+                   'parallelism': 'env-sharded x%d (no collective)' % world},
+        'roofline': {'bound': 'mfma', 'achieved': achieved, 'peak': MFMA_F64_PEAK_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': achieved / MFMA_F64_PEAK_TFLOPS,
+                     'traffic': None, 'kernel': 'ce::' + eng.step_kernel,
+                     'flops_per_env_step': flops, 'kernel_ms_median': kernel_ms,
+                     'kernel_ms_mean': kernel_ms_mean,
+                     'note': 'algorithmic GEMM flops; the kernel pads K 10 -> 16 and F 49 -> '
+                             '52 (forward) / 64 (gradient) on 16x16x4 MFMA tiles'},
     })
     return line
 

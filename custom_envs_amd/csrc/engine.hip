@@ -23,6 +23,7 @@
 #include "common.h"
 #include "mlp_kernels.h"
 #include "optimize_kernels.h"
+#include "optimize_mfma_kernel.h"
 #include "optimize_pair_kernel.h"
 #include "seeding.h"
 
@@ -54,6 +55,36 @@ template <typename T, int F, int K>
 void launch_reset(const void *args, int grid, size_t, hipStream_t stream) {
     hipLaunchKernelGGL((ce::optimize_reset_kernel<T, F, K>), dim3(grid), dim3(ce::kBlock), 0,
                        stream, *static_cast<const ce::StepArgs<T> *>(args));
+}
+
+// Any (F <= 64, K <= 16) shape on the f64 matrix cores (optimize_mfma_kernel.h).
+template <int FT>
+void launch_gen(const void *args, int, size_t lds, hipStream_t stream) {
+    const auto &a = *static_cast<const ce::StepArgs<double> *>(args);
+    const int grid = (a.E + ce::kGenWaves - 1) / ce::kGenWaves;
+    hipLaunchKernelGGL((ce::optimize_mfma_kernel<FT>), dim3(grid), dim3(ce::kGenBlock), lds,
+                       stream, a);
+}
+
+void launch_gen_reset(const void *args, int, size_t, hipStream_t stream) {
+    const auto &a = *static_cast<const ce::StepArgs<double> *>(args);
+    const int grid = (a.E + ce::kGenResetWaves - 1) / ce::kGenResetWaves;
+    hipLaunchKernelGGL(ce::optimize_reset_rt_kernel, dim3(grid),
+                       dim3(ce::kWave * ce::kGenResetWaves), 0, stream, a);
+}
+
+const StepFn kGenSteps[ce::kGenMaxFT] = {launch_gen<1>, launch_gen<2>, launch_gen<3>,
+                                         launch_gen<4>};
+
+int set_gen_lds_limits() {
+    const void *fns[ce::kGenMaxFT] = {reinterpret_cast<const void *>(ce::optimize_mfma_kernel<1>),
+                                      reinterpret_cast<const void *>(ce::optimize_mfma_kernel<2>),
+                                      reinterpret_cast<const void *>(ce::optimize_mfma_kernel<3>),
+                                      reinterpret_cast<const void *>(ce::optimize_mfma_kernel<4>)};
+    for (int t = 0; t < ce::kGenMaxFT; ++t)
+        CE_HIP(hipFuncSetAttribute(fns[t], hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   static_cast<int>(2 * ce::gen_block_bytes(t + 1))));
+    return CE_OK;
 }
 
 struct KernelEntry {
@@ -114,6 +145,7 @@ struct ce_engine {
     bool was_reset = false;
     bool staged = false;      // dataset fits the per-block LDS stage
     StepFn pair = nullptr;    // two-envs-per-wave step kernel, when the shape has one
+    int gen_ft = 0;           // > 0: the runtime-shape MFMA kernel with this many feature tiles
     std::string kernel_name;  // what ce_step_kernel reports
     size_t stage_bytes = 0;
     ce::GraphCache graphs;   // ce_step_many
@@ -141,6 +173,8 @@ ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs
     a.B = e->cfg.batch_size;
     a.max_steps = e->cfg.max_steps;
     a.auto_reset = e->cfg.auto_reset;
+    a.F = e->cfg.n_features;
+    a.K = e->cfg.n_classes;
     a.data = static_cast<const unsigned char *>(e->X);
     a.W = static_cast<T *>(e->W);
     a.G = static_cast<T *>(e->G);
@@ -206,6 +240,14 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
             if (e->mlp_phases & 1) hipLaunchKernelGGL(ce::mlp_train_kernel, grid, block, 0, stream, a);
             if (e->mlp_phases & 2) hipLaunchKernelGGL(ce::mlp_info_kernel, grid, block, 0, stream, a);
         }
+        return;
+    }
+    if (e->gen_ft) {
+        auto a = make_args<double>(e, act, o);
+        if (reset)
+            launch_gen_reset(&a, 0, 0, stream);
+        else
+            kGenSteps[e->gen_ft - 1](&a, 0, 2 * ce::gen_block_bytes(e->gen_ft), stream);
         return;
     }
     StepFn fn = reset ? e->kern->reset
@@ -341,11 +383,21 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
                                          "n_rows, n_rows % 64 == 0, n_features % 8 == 0, "
                                          "n_classes <= 16");
     } else {
-        kern = find_kernel(cfg->precision, cfg->n_features, cfg->n_classes);
-        if (!kern)
-            return fail(CE_EUNSUPPORTED, "ce_create: no compiled kernel for F=" +
-                                             std::to_string(cfg->n_features) +
-                                             " K=" + std::to_string(cfg->n_classes));
+        // a register-path instance when the shape has one (unless CE_GENERIC=1
+        // forces the runtime-shape kernel, for tests), else the MFMA kernel
+        const char *force = std::getenv("CE_GENERIC");
+        if (!(force && force[0] == '1'))
+            kern = find_kernel(cfg->precision, cfg->n_features, cfg->n_classes);
+        if (!kern) {
+            if (cfg->precision != CE_F64 || cfg->n_features > 16 * ce::kGenMaxFT ||
+                cfg->n_classes > ce::kGenMaxK)
+                return fail(CE_EUNSUPPORTED,
+                            "ce_create: no kernel for F=" + std::to_string(cfg->n_features) +
+                                " K=" + std::to_string(cfg->n_classes) +
+                                (cfg->precision != CE_F64
+                                     ? " in float32 (any F <= 64, K <= 16 runs in float64)"
+                                     : " (the float64 MFMA kernel takes F <= 64, K <= 16)"));
+        }
     }
     for (int i = 0; i < cfg->n_rows; ++i)
         if (labels[i] < 0 || labels[i] >= cfg->n_classes)
@@ -393,6 +445,11 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         CE_TRY(hipMalloc(&e->X, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->Xs, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
+    } else if (!kern) {
+        e->gen_ft = ce::gen_ft(cfg->n_features);
+        CE_TRY(hipMalloc(&e->X, static_cast<size_t>(ce::gen_rows_padded(cfg->n_rows)) *
+                                    ce::gen_stride(e->gen_ft) * sizeof(double)));
+        if (set_gen_lds_limits() != CE_OK) return bail(CE_EHIP);
     } else {
         CE_TRY(hipMalloc(&e->X, ce::stage_bytes_total(cfg->n_features, cfg->n_rows,
                                                       static_cast<int>(e->tsize))));
@@ -449,7 +506,22 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         CE_TRY(hipMemcpy(e->label, labels, N * sizeof(int32_t), hipMemcpyHostToDevice));
     }
 #undef CE_TRY
-    if (!mlp) {
+    if (e->gen_ft) {
+        // [Npad][RS] float64: F features, zeros to 16 FT + 1, the label as a
+        // double in the last column; rows N..Npad-1 are zeros with label -1
+        const int RS = ce::gen_stride(e->gen_ft);
+        const size_t npad = ce::gen_rows_padded(cfg->n_rows);
+        std::vector<double> img(npad * RS, 0.0);
+        for (size_t r = 0; r < npad; ++r) {
+            if (r < N)
+                for (size_t f = 0; f < F; ++f) img[r * RS + f] = features[r * F + f];
+            img[r * RS + RS - 1] = r < N ? static_cast<double>(labels[r]) : -1.0;
+        }
+        if (hipMemcpy(e->X, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice) !=
+            hipSuccess)
+            return bail(fail(CE_EHIP, "ce_create: dataset upload failed"));
+        e->kernel_name = "optimize_mfma_kernel<" + std::to_string(e->gen_ft) + ">";
+    } else if (!mlp) {
     // [rows | labels]: row-major rows padded to ce::row_stride elements (zeros
     // in the pad), then the int32 labels, in one buffer staged with one copy.
     // Two-class shapes store s_y x with s_y = +1 (y = 0) / -1 (y = 1)

@@ -72,6 +72,7 @@ struct MathConsts {};
 template <typename T>
 struct StepArgs {
     int E, N, B, max_steps, auto_reset;
+    int F, K;                   // features, classes (the runtime-shape kernel reads them)
     const unsigned char *data;  // [N][RS] rows (padded, row_stride) then [N] int32 labels
     T *W;                  // [E][P] model.weights
     T *G;                  // [E][P] grad_hist[idx] of the last step

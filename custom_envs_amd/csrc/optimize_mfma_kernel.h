@@ -1,0 +1,325 @@
+// Optimize-v0 step for any data-set shape on the f64 matrix cores (gfx950).
+//
+// The register-path kernels (optimize_kernels.h, optimize_pair_kernel.h)
+// are compiled per (F, K) and keep a whole dataset in one workgroup's LDS.
+// The reference's default data sets do not fit that: load_data('mnist' |
+// 'fashion' | 'emnist-digits') is 60,000 rows of 7x7 = 49 features and 10
+// classes (custom_envs/data/load_data.py:65-97; Optimize.__init__ defaults
+// to data_set='mnist', batch_size=None, custom_envs/envs/optimize.py:40), so
+// one step of one env is X_b W (N x 49 x 10), a softmax, and X_b^T (P - Y)
+// (optimize.py:74-78, the build-defined ModelNumpy): two dense
+// GEMMs.  This kernel runs them on v_mfma_f64_16x16x4_f64 for any F <= 64,
+// K <= 16, N and B, in float64 (the reference's dtype).
+//
+// Mapping: one wave per env, kGenWaves envs per workgroup.  The dataset
+// streams through LDS in blocks of 64 rows (LDS-DMA, double-buffered), so
+// one HBM/L2 read of a block serves the workgroup's 8 envs.  Per 16-row
+// sub-block and env:
+//   forward   Z (16 rows x 16 classes) = X (16 x 4nk) . W' (4nk x 16):
+//             nk = ceil(F/4) MFMAs; A = X[row l&15][4k + l>>4] from LDS,
+//             B = W'[4k + l>>4][l&15] held in registers for the whole step.
+//   softmax   f64 MFMA C layout: lane l holds class l&15 of rows
+//             (l>>4) + 4r, r = 0..3, so a row's classes are one 16-lane DPP
+//             row: max / sum / first-argmax are 4 xor-shuffle levels each.
+//   gradient  G (16 features x 16 classes) += X^T (16 x 4 rows) . D (4 rows
+//             x 16 classes) per feature tile: D = P - Y straight from the
+//             softmax registers -- C register r of lane l is row 4r + (l>>4),
+//             class l&15, exactly the B operand of k-step r -- and
+//             A = X[row 4r + (l>>4)][16 ft + (l&15)] from LDS: 4 * ceil(F/16)
+//             MFMAs, no cross-lane reduction (the row sum is the MFMA's k).
+// Minibatches (B < N) gather their B rows per env through the env's row
+// order straight from HBM/L2; the full-data info pass (optimize.py:94-97)
+// is then the LDS stream without the gradient.  With B == N the reference
+// computes the same numbers twice; they are reused.
+// Cross-entropy is -log(p_y + 1e-16) per row (utils_math.py:25-34), taken
+// as -log of per-lane products folded before they can underflow; the
+// argmax is np.argmax's first maximum of P.
+#pragma once
+
+#include "optimize_kernels.h"
+
+namespace ce {
+
+typedef double gen_d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kGenWaves = 8;                   // envs per workgroup, one wave each
+constexpr int kGenBlock = kWave * kGenWaves;
+constexpr int kGenRows = 64;                   // dataset rows per LDS block
+constexpr int kGenMaxFT = 4;                   // feature tiles of 16: F <= 64
+constexpr int kGenMaxK = 16;                   // classes: one 16-wide tile
+constexpr int kGenResetWaves = 16;
+
+__host__ __device__ constexpr int gen_ft(int F) { return (F + 15) / 16; }
+// float64 per stored row: 16 FT features (zero-padded), one pad, the label
+// (as a double; -1 marks the rows that pad N up to a whole block).  An odd
+// number of 16-byte units keeps the forward's A reads conflict-free.
+__host__ __device__ constexpr int gen_stride(int ft) { return 16 * ft + 2; }
+__host__ __device__ constexpr size_t gen_block_bytes(int ft) {
+    return static_cast<size_t>(kGenRows) * gen_stride(ft) * sizeof(double);
+}
+__host__ __device__ constexpr int gen_rows_padded(int N) {
+    return (N + kGenRows - 1) / kGenRows * kGenRows;
+}
+
+// 16-lane (one DPP row) reductions: xor 1, 2, 4, 8.
+__device__ __forceinline__ double row_max16(double v) {
+    v = fmax(v, xchg<1>(v));
+    v = fmax(v, xchg<2>(v));
+    v = fmax(v, xchg<4>(v));
+    return fmax(v, xchg<8>(v));
+}
+__device__ __forceinline__ double row_min16(double v) {
+    v = fmin(v, xchg<1>(v));
+    v = fmin(v, xchg<2>(v));
+    v = fmin(v, xchg<4>(v));
+    return fmin(v, xchg<8>(v));
+}
+__device__ __forceinline__ double row_sum16(double v) { return lane_sum<double, 8>(v); }
+
+// One (row, class) entry of the softmax classifier (utils_math.py:51-63,
+// 25-34 and the A7 model): returns P - Y for the gradient (0 for padded
+// rows / classes) and adds the row's cross-entropy factor and argmax hit on
+// the lane holding the row's label.
+__device__ __forceinline__ double gen_softmax(double z, int c, int K, int y, double &prod,
+                                              int &hits) {
+    const bool cls = c < K;
+    const bool valid = y >= 0;
+    const double m = row_max16(cls ? z : -INFINITY);
+    const double ex = cls ? exp_neg(m - z, MathConsts<double>()) : 0.0;   // exp(z - max)
+    const double s = row_sum16(ex);
+    const double p = ex / s;
+    const double pm = row_max16(cls ? p : -1.0);
+    const double first = row_min16((cls && p == pm) ? static_cast<double>(c) : 99.0);
+    const bool own = valid && c == y;
+    hits += (own && first == static_cast<double>(y)) ? 1 : 0;
+    prod *= own ? p + 1e-16 : 1.0;
+    return (valid && cls) ? p - (c == y ? 1.0 : 0.0) : 0.0;
+}
+
+__device__ __forceinline__ void gen_fold(double &loss, double &prod) {
+    // factors are in (1e-16, 1]: fold long before the product can underflow
+    if (__any(prod < 1e-200)) {
+        loss -= log_pos(prod);
+        prod = 1.0;
+    }
+}
+
+// W <- W0, histories <- 0, current_step <- 0, order <- order[perm]
+// (optimize.py:58-67) for a runtime parameter count.
+__device__ __forceinline__ void reset_env_rt(const StepArgs<double> &a, int e, int lane, int P) {
+    const size_t base = static_cast<size_t>(e) * P;
+    for (int i = lane; i < P; i += kWave) {
+        a.W[base + i] = a.W0[base + i];
+        a.G[base + i] = 0.0;
+    }
+    if (lane == 0) {
+        a.L[e] = 0.0;
+        a.step[e] = 0;
+    }
+    if (a.order != nullptr) {
+        const int sel = a.order_sel[e];
+        const size_t stride = static_cast<size_t>(a.E) * a.N;
+        const int32_t *cur = a.order + sel * stride + static_cast<size_t>(e) * a.N;
+        int32_t *nxt = a.order + (1 - sel) * stride + static_cast<size_t>(e) * a.N;
+        const int32_t *pm = a.perm + static_cast<size_t>(e) * a.N;
+        for (int i = lane; i < a.N; i += kWave) nxt[i] = cur[pm[i]];
+        if (lane == 0) a.order_sel[e] = 1 - sel;
+    }
+}
+
+__global__ __launch_bounds__(kWave *kGenResetWaves) void optimize_reset_rt_kernel(
+    StepArgs<double> a) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int e = blockIdx.x * kGenResetWaves + (threadIdx.x >> 6);
+    if (e >= a.E) return;
+    const int P = a.F * a.K;
+    reset_env_rt(a, e, lane, P);
+    float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
+    for (int i = lane; i < 2 * P + 1; i += kWave) obs[i] = 0.0f;
+}
+
+template <int FT>
+__global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<double> a) {
+    constexpr int RS = gen_stride(FT);
+    constexpr int NK = 4 * FT;                       // forward k-steps at most
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int e = blockIdx.x * kGenWaves + wave;
+    const bool active = e < a.E;                     // wave-uniform
+    const int eidx = active ? e : 0;
+    const int F = a.F, K = a.K, P = F * K, N = a.N, B = a.B;
+    const int nk = (F + 3) >> 2;
+    const int c = lane & 15, h = lane >> 4;
+    const double *X = reinterpret_cast<const double *>(a.data);
+    const size_t pbase = static_cast<size_t>(eidx) * P;
+
+    // ---- state: W' = W - a (optimize.py:74-75) as the forward's B operands
+    const int step_prev = a.step[eidx];
+    const double lprev = a.L[eidx];
+    double wb[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        const int f = 4 * k + h;
+        const bool own = f < F && c < K;
+        const int idx = own ? f * K + c : 0;
+        const double w = a.W[pbase + idx] - static_cast<double>(a.act[pbase + idx]);
+        wb[k] = own ? w : 0.0;
+    }
+
+    gen_d4 g[FT];
+#pragma unroll
+    for (int t = 0; t < FT; ++t) g[t] = gen_d4{0.0, 0.0, 0.0, 0.0};
+    double loss = 0.0, prod = 1.0;       // minibatch cross-entropy partials
+    int hits = 0;
+    double floss = 0.0, fprod = 1.0;     // info pass (B < N)
+    int fhits = 0;
+    const bool full = B == N;
+
+    // ---- minibatch B < N: sequence[0] = rows [0, B) of the env's order
+    if (!full && active) {
+        const int sel = a.order_sel[e];
+        const int32_t *order = a.order + sel * static_cast<size_t>(a.E) * N +
+                               static_cast<size_t>(e) * N;
+        for (int i0 = 0; i0 < B; i0 += 16) {
+            const int ia = i0 + c;
+            const double *xa = X + static_cast<size_t>(ia < B ? order[ia] : 0) * RS;
+            const bool va = ia < B;
+            gen_d4 z = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < NK; ++k)
+                if (k < nk)
+                    z = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? xa[4 * k + h] : 0.0, wb[k], z,
+                                                             0, 0, 0);
+            const double *xr[4];
+            double d[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ir = i0 + h + 4 * r;
+                xr[r] = X + static_cast<size_t>(ir < B ? order[ir] : 0) * RS;
+                const int y = ir < B ? static_cast<int>(xr[r][RS - 1]) : -1;
+                d[r] = gen_softmax(z[r], c, K, y, prod, hits);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int t = 0; t < FT; ++t)
+                    g[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[r][16 * t + c], d[r], g[t], 0,
+                                                                0, 0);
+            gen_fold(loss, prod);
+        }
+    }
+
+    // ---- every row, streamed through LDS (forward [+ gradient when B == N])
+    const int nblk = gen_rows_padded(N) / kGenRows;
+    constexpr size_t kBlk = gen_block_bytes(FT);
+    constexpr int kVec = static_cast<int>(kBlk / 16);
+    constexpr int kChunks = (kVec + kWave - 1) / kWave;
+    auto stage = [&](int j, int buf) {
+        // LDS-DMA: one wave instruction moves 1 KiB straight into LDS
+        const unsigned char *src = a.data + static_cast<size_t>(j) * kBlk;
+        unsigned char *dst = smem + buf * kBlk;
+        for (int ch = wave; ch < kChunks; ch += kGenWaves) {
+            const int v = ch * kWave + lane;
+            if (v < kVec)
+                __builtin_amdgcn_global_load_lds(
+                    (__attribute__((address_space(1))) void *)(src + static_cast<size_t>(v) * 16),
+                    (__attribute__((address_space(3))) void *)(dst + ch * kWave * 16), 16, 0, 0);
+        }
+    };
+    stage(0, 0);
+    for (int j = 0; j < nblk; ++j) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's part of block j
+        __syncthreads();                                   // everyone's; block j-1 consumed
+        if (j + 1 < nblk) stage(j + 1, (j + 1) & 1);
+        if (active) {
+            const double *xb = reinterpret_cast<const double *>(smem + (j & 1) * kBlk);
+#pragma unroll 1
+            for (int sb = 0; sb < kGenRows / 16; ++sb) {
+                const double *xs = xb + sb * 16 * RS;
+                gen_d4 z = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k = 0; k < NK; ++k)
+                    if (k < nk)
+                        z = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[c * RS + 4 * k + h], wb[k], z,
+                                                                 0, 0, 0);
+                double d[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int y = static_cast<int>(xs[(h + 4 * r) * RS + RS - 1]);
+                    if (full)
+                        d[r] = gen_softmax(z[r], c, K, y, prod, hits);
+                    else
+                        d[r] = gen_softmax(z[r], c, K, y, fprod, fhits);
+                }
+                if (full) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int t = 0; t < FT; ++t)
+                            g[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                                xs[(h + 4 * r) * RS + 16 * t + c], d[r], g[t], 0, 0, 0);
+                    gen_fold(loss, prod);
+                } else {
+                    gen_fold(floss, fprod);
+                }
+            }
+        }
+    }
+    if (!active) return;
+
+    // ---- totals
+    loss -= log_pos(prod);
+    const double mb_loss = wave_sum(loss) / B;
+    const double mb_acc = wave_sum(static_cast<double>(hits)) / B;
+    double objective = mb_loss, accuracy = mb_acc;
+    if (!full) {
+        floss -= log_pos(fprod);
+        objective = wave_sum(floss) / N;
+        accuracy = wave_sum(static_cast<double>(fhits)) / N;
+    }
+
+    // ---- recurrences (optimize.py:78-92) and outputs
+    const int cur_step = step_prev + 1;
+    const double lnew = (mb_loss - lprev) / (lprev + 0.1);
+    const bool done = cur_step >= a.max_steps;
+    const bool wipe = done && a.auto_reset;
+    const int OBS = 2 * P + 1;
+    float *obs = a.obs + static_cast<size_t>(e) * OBS;
+#pragma unroll
+    for (int t = 0; t < FT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f = 16 * t + h + 4 * q;       // C row of register q
+            if (f < F && c < K) {
+                const int idx = f * K + c;
+                const double gp = a.G[pbase + idx];
+                const double gn = (g[t][q] / B) / (fabs(gp) + 1.0);
+                if (!wipe) a.G[pbase + idx] = gn;
+                obs[P + 1 + idx] = wipe ? 0.0f : static_cast<float>(gn);
+            }
+        }
+    if (!wipe) {
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int f = 4 * k + h;
+            if (k < nk && f < F && c < K) a.W[pbase + f * K + c] = wb[k];
+        }
+    }
+    for (int i = lane; i < P; i += kWave) obs[i] = 0.0f;   // wght_hist is identically 0
+    if (lane == 0) {
+        obs[P] = wipe ? 0.0f : static_cast<float>(lnew);
+        a.reward[e] = static_cast<float>(-mb_loss);
+        a.done[e] = done ? 1 : 0;
+        a.objective[e] = static_cast<float>(objective);
+        a.accuracy[e] = static_cast<float>(accuracy);
+        a.episode_len[e] = cur_step;
+        if (!wipe) {
+            a.L[e] = lnew;
+            a.step[e] = cur_step;
+        }
+    }
+    if (wipe) reset_env_rt(a, e, lane, P);
+}
+
+}  // namespace ce

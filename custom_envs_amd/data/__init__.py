@@ -1,7 +1,9 @@
-"""Dataset loaders (custom_envs/data/load_data.py:47-112), synthetic only.
+"""Dataset loaders (custom_envs/data/load_data.py:47-112).
 
-Every real data file in the reference (iris.npz, the MNIST/EMNIST/fashion
-IDX archives) is a git-LFS pointer, so only the synthetic sets are served:
+The file-backed sets ('mnist', 'mnist-test', 'fashion', 'emnist-digits',
+'iris', 'skin') read files a user supplies (``data_dir`` or
+$CUSTOM_ENVS_DATA_DIR; data/files.py): every data file in the reference is a
+git-LFS pointer.  Built in, no files needed:
 
   random_gaussians   sklearn make_classification() + one-hot(2), exactly the
                      reference's branch (load_data.py:105-107)
@@ -11,6 +13,11 @@ IDX archives) is a git-LFS pointer, so only the synthetic sets are served:
   mnist_synthetic    "MNIST-sized" features for the MLP config:
                      RandomState(0).rand(1024, 784), labels argmax(X T) with
                      T = RandomState(1).normal(size=(784, 10))
+  mnist7x7_synthetic the shape load_data('mnist') gives (60,000 rows of
+                     7x7 = 49 features in [0, 1], 10 classes): synthetic
+                     28x28 uint8 "digits" (class-dependent blobs + noise)
+                     sampled at the PIL NEAREST 28 -> 7 pixels, normalised
+                     as the mnist branch does (load_data.py:65-71)
   iris_synthetic     iris-shaped stand-in for 'iris' (load_data's default,
                      the data set of get_problem('nn')): 150 rows, 4
                      features, 3 classes of 50, Gaussian blobs at the iris
@@ -45,6 +52,19 @@ def _mnist_synthetic(num_of_labels=None):
     return features, to_onehot(labels, num_of_labels or 10)[0]
 
 
+def _mnist7x7_synthetic(num_of_labels=None, n_rows=60000, seed=0):
+    rs = np.random.RandomState(seed)
+    labels = rs.randint(0, 10, n_rows)
+    pos = np.arange(2, 28, 4).astype(np.float64)         # NEAREST 28 -> 7 samples
+    cy = (6 + 2 * (labels % 5) + rs.randint(-3, 4, n_rows))[:, None, None]
+    cx = (7 + 3 * (labels // 5) + rs.randint(-3, 4, n_rows))[:, None, None]
+    sig = (3.0 + labels % 3)[:, None, None]
+    r2 = (pos[None, :, None] - cy) ** 2 + (pos[None, None, :] - cx) ** 2
+    img = 255 * np.exp(-r2 / (2 * sig ** 2)) + rs.normal(0, 24, (n_rows, 7, 7))
+    img = np.clip(np.round(img), 0, 255).astype(np.uint8).reshape(n_rows, 49)
+    return normalize(img), to_onehot(labels, num_of_labels)[0]
+
+
 def normalize(data):
     """utils_math.py:77-87: per column (x - min) / (max - min + 1e-8)."""
     mins, maxes = np.min(data, axis=0), np.max(data, axis=0)
@@ -69,6 +89,7 @@ LOADERS = {
     'gaussians_256x10': lambda n: _gaussians(n_samples=256, n_features=10, random_state=0),
     'mnist_synthetic': _mnist_synthetic,
     'iris_synthetic': _iris_synthetic,
+    'mnist7x7_synthetic': _mnist7x7_synthetic,
 }
 
 
@@ -76,12 +97,15 @@ def load_data(name='gaussians_256x10', batch_size=32, num_of_labels=None, data_d
     """Return an ``InMemoryDataSet`` (load_data.py:47-112 signature).
 
     The file-backed sets ('mnist', 'mnist-test', 'fashion', 'emnist-digits',
-    'iris', 'skin'; custom_envs_amd/data/files.py) read ``data_dir``, laid out
+    'iris', 'skin'; custom_envs_amd/data/files.py) read ``data_dir`` (default:
+    the CUSTOM_ENVS_DATA_DIR environment variable), laid out
     as the reference's custom_envs/data/ directory; the reference's own copies
     are git-LFS pointers and are refused.  'cifar-10' needs a keras download
     and is not served."""
+    import os
     from custom_envs_amd.data import files
     if name in files.IDX_SETS + files.TABLE_SETS:
+        data_dir = data_dir or os.environ.get('CUSTOM_ENVS_DATA_DIR')
         if data_dir is None:
             raise RuntimeError('data set %r reads files: pass data_dir (the reference ships '
                                'them as git-LFS pointers)' % name)

@@ -60,13 +60,13 @@ class GPUVecEnv:
 
     def __init__(self, num_envs, data_set='gaussians_256x10', batch_size=None,
                  n_of_steps=None, max_steps=40, precision=None, device=0, seed=None,
-                 model='linear', hidden=64, monitor=None):
+                 model='linear', hidden=64, monitor=None, data_dir=None):
         """``monitor``: None, or (file paths, Monitor keywords) -- the batched
         form of wrapping every env in utils_logging.Monitor
         (utils_logging.py:159-175); writes the same ``.mon.csv`` chunks."""
         from custom_envs_amd.engine import OptimizeEngine
         from custom_envs_amd.utils.utils_logging import VecMonitor
-        features, targets = resolve_dataset(data_set, batch_size)
+        features, targets = resolve_dataset(data_set, batch_size, data_dir)
         self.engine = OptimizeEngine(features, targets, num_envs, batch_size=batch_size,
                                      max_steps=max_steps, precision=precision, device=device,
                                      auto_reset=True, model=model, hidden=hidden)

@@ -1,0 +1,178 @@
+"""The runtime-shape f64 MFMA step kernel (optimize_mfma_kernel.h) against
+the CPU oracle: the reference's own image-set shape (7x7 = 49 features, 10
+classes; load_data('mnist'), optimize.py:40) through the real IDX loader,
+ragged N (padded LDS blocks), minibatches, every feature-tile count, the
+largest K, odd env counts (a partial workgroup), across auto-resets; and the
+shapes the register kernels serve, forced onto this kernel (CE_GENERIC=1).
+Tolerance as test_gpu_parity.py: float64 results rounded to float32 within
+1e-6 relative (atol 1e-9), accuracy exact."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+from oracle.optimize import Optimize as OracleEnv
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a ROCm device (run under gpurun)')
+
+
+def _engine(dataset, num_envs, batch_size=None, generic=False, **kw):
+    from custom_envs_amd.engine import OptimizeEngine
+    old = os.environ.get('CE_GENERIC')
+    os.environ['CE_GENERIC'] = '1' if generic else '0'
+    try:
+        return OptimizeEngine(*dataset, num_envs=num_envs, batch_size=batch_size, **kw)
+    finally:
+        if old is None:
+            os.environ.pop('CE_GENERIC')
+        else:
+            os.environ['CE_GENERIC'] = old
+
+
+def _classes(n_rows, n_features, n_classes, seed):
+    rs = np.random.RandomState(seed)
+    centers = rs.normal(0, 1.0, (n_classes, n_features))
+    y = rs.randint(0, n_classes, n_rows)
+    x = centers[y] + rs.normal(0, 1.0, (n_rows, n_features))
+    return x, np.eye(n_classes)[y]
+
+
+def _check(dataset, batch_size, eng, envs, steps, seed0=11, scale=0.02):
+    E, P = eng.num_envs, eng.act_dim
+    seeds = [seed0 + 3 * i for i in range(E)]
+    acts = np.random.RandomState(E + P).normal(0, scale, (steps, E, P)).astype(np.float32)
+    eng.seed(seeds)
+    assert np.all(eng.reset() == 0)
+    refs = {}
+    for i in envs:
+        env = OracleEnv(*dataset, batch_size=batch_size)
+        env.seed(seeds[i])
+        env.reset()
+        refs[i] = env
+    for t in range(steps):
+        out = eng.step(acts[t])
+        for i, env in refs.items():
+            obs, rew, done, info = env.step(acts[t, i])
+            if done:
+                obs = env.reset()
+            assert bool(out['done'][i]) == done, (i, t)
+            assert out['episode_len'][i] == info['episode']['l']
+            np.testing.assert_allclose(out['obs'][i], obs, rtol=1e-6, atol=1e-9,
+                                       err_msg='env %d step %d' % (i, t))
+            assert out['reward'][i] == pytest.approx(rew, rel=1e-6)
+            assert out['objective'][i] == pytest.approx(info['objective'], rel=1e-6)
+            assert out['accuracy'][i] == np.float32(info['accuracy']), (i, t)
+    return refs
+
+
+def test_mnist_idx_fixture_through_make():
+    """make('Optimize-v0', data_set='mnist', data_dir=...) on the committed
+    synthetic IDX files: the reference's default data set shape (F = 49,
+    K = 10) runs, on the MFMA kernel, and matches the oracle."""
+    from custom_envs_amd import make
+    from custom_envs_amd.data import load_data
+    data_dir = os.path.join(GOLDEN, 'idx')
+    env = make('Optimize-v0', data_set='mnist', data_dir=data_dir)
+    assert env.engine.step_kernel == 'optimize_mfma_kernel<4>'
+    assert env.observation_space.shape == (2 * 490 + 1,) and env.action_space.shape == (490,)
+    seq = load_data('mnist', batch_size=None, data_dir=data_dir)
+    ref = OracleEnv(seq.features, seq.targets)
+    env.seed(3)
+    ref.seed(3)
+    np.testing.assert_array_equal(env.reset(), ref.reset())
+    acts = np.random.RandomState(0).normal(0, 0.05, (42, 490)).astype(np.float32)
+    for t in range(42):
+        obs, rew, done, info = env.step(acts[t])
+        robs, rrew, rdone, rinfo = ref.step(acts[t])
+        assert done == rdone and info['episode']['l'] == rinfo['episode']['l']
+        np.testing.assert_allclose(obs, robs, rtol=1e-6, atol=1e-9)
+        assert rew == pytest.approx(rrew, rel=1e-6)
+        assert info['accuracy'] == np.float32(rinfo['accuracy'])
+        if done:
+            break
+    env.close()
+
+
+@pytest.mark.parametrize('batch_size', [None, 32, 100])
+def test_image_shape_many_envs(batch_size):
+    """49 x 10 at N = 1000 (not a multiple of the 64-row block), 13 envs
+    (one full and one partial workgroup), 43 steps across an auto-reset."""
+    ds = _classes(1000, 49, 10, 1)
+    eng = _engine(ds, 13, batch_size)
+    assert eng.step_kernel == 'optimize_mfma_kernel<4>'
+    _check(ds, batch_size, eng, [0, 7, 8, 12], 43)
+    eng.close()
+
+
+@pytest.mark.parametrize('shape', [(4, 3), (17, 2), (33, 7), (64, 16), (49, 10), (1, 5)])
+def test_every_feature_tile_count(shape):
+    F, K = shape
+    ds = _classes(300, F, K, F + K)
+    eng = _engine(ds, 9, None)
+    assert eng.step_kernel == 'optimize_mfma_kernel<%d>' % ((F + 15) // 16)
+    _check(ds, None, eng, [0, 8], 41)
+    eng.close()
+
+
+@pytest.mark.parametrize('batch_size', [None, 32])
+def test_register_shapes_forced_generic(lr_dataset, batch_size):
+    """The benchmark shape (256 x 10, K = 2) on the MFMA kernel agrees with
+    the oracle as the register kernels do."""
+    eng = _engine(lr_dataset, 10, batch_size, generic=True)
+    assert eng.step_kernel == 'optimize_mfma_kernel<1>'
+    _check(lr_dataset, batch_size, eng, [0, 9], 42)
+    eng.close()
+
+
+@pytest.mark.parametrize('name', ['ref_optimize_s0', 'ref_optimize_b32_s3'])
+def test_generic_vs_reference_code(lr_dataset, name):
+    fx = golden(name + '.npz')
+    bs = int(fx['batch_size'])
+    eng = _engine(lr_dataset, 1, None if bs < 0 else bs, generic=True)
+    eng.seed([int(fx['seed'])])
+    eng.reset()
+    for t in range(fx['actions'].shape[0]):
+        out = eng.step(fx['actions'][t][None])
+        assert bool(out['done'][0]) == bool(fx['done'][t])
+        np.testing.assert_allclose(out['obs'][0], fx['obs'][t], rtol=1e-6, atol=1e-9)
+        assert out['accuracy'][0] == np.float32(fx['accuracy'][t])
+    eng.close()
+
+
+def test_state_roundtrip_and_device_path():
+    """get/set_state and the device-pointer path on the MFMA kernel."""
+    import torch
+    ds = _classes(200, 49, 10, 7)
+    eng = _engine(ds, 5, 32)
+    eng.seed(list(range(5)))
+    eng.reset()
+    acts = np.random.RandomState(1).normal(0, 0.02, (3, 5, 490)).astype(np.float32)
+    for t in range(3):
+        eng.step(acts[t])
+    st = eng.get_state()
+    host = {k: v.copy() for k, v in eng.step(acts[0]).items()}
+    eng.set_state(**st)
+    out = eng.alloc_device_outputs()
+    eng.step_device(torch.from_numpy(acts[0]).cuda(), out)
+    eng.wait()
+    np.testing.assert_array_equal(out['obs'].cpu().numpy(), host['obs'])
+    np.testing.assert_array_equal(out['accuracy'].cpu().numpy(), host['accuracy'])
+    eng.close()
+
+
+def test_unsupported_shapes_fail_loudly():
+    from custom_envs_amd._native import NativeEngineError
+    ds = _classes(64, 65, 3, 0)
+    with pytest.raises(NativeEngineError, match='F <= 64'):
+        _engine(ds, 2)
+    ds = _classes(64, 49, 10, 0)
+    with pytest.raises(NativeEngineError, match='float64'):
+        _engine(ds, 2, precision='f32')

@@ -81,10 +81,11 @@ def test_bad_arguments_are_reported():
 
 
 def test_unsupported_shape_is_loud():
+    """Beyond the f64 MFMA kernel's F <= 64, K <= 16 (any other shape runs)."""
     lib = _native.load()
     cfg = _native.CeConfig(abi_version=_native.ABI_VERSION, num_envs=1, n_rows=4,
-                           n_features=7, n_classes=5, batch_size=4, max_steps=40)
-    x = np.zeros((4, 7))
+                           n_features=65, n_classes=5, batch_size=4, max_steps=40)
+    x = np.zeros((4, 65))
     y = np.zeros(4, np.int32)
     handle = ctypes.c_void_p()
     assert lib.ce_create(ctypes.byref(cfg), x.ctypes.data, y.ctypes.data,
