@@ -116,7 +116,7 @@ def test_image_shape_many_envs(batch_size):
 def test_every_feature_tile_count(shape):
     F, K = shape
     ds = _classes(300, F, K, F + K)
-    eng = _engine(ds, 9, None)
+    eng = _engine(ds, 9, None, generic=True)
     assert eng.step_kernel == 'optimize_mfma_kernel<%d>' % ((F + 15) // 16)
     _check(ds, None, eng, [0, 8], 41)
     eng.close()
