@@ -28,12 +28,13 @@ def _hipcc():
 
 
 def sources():
-    return [os.path.join(CSRC, f) for f in ('engine.hip', 'multi_engine.hip', 'multinn_engine.hip', 'seeding.cpp')]
+    return [os.path.join(CSRC, f) for f in ('engine.hip', 'optimize_mfma.hip', 'multi_engine.hip',
+                                            'multinn_engine.hip', 'seeding.cpp')]
 
 
 def headers():
     return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'optimize_pair_kernel.h',
-                                            'optimize_mfma_kernel.h',
+                                            'optimize_mfma_kernel.h', 'optimize_mfma.h',
                                             'multiopt_kernels.h', 'mlp_kernels.h', 'multinn_kernels.h', 'common.h', 'seeding.h')] + [
         os.path.join(ROOT, 'include', 'custom_envs_amd.h')]
 

@@ -23,7 +23,7 @@
 #include "common.h"
 #include "mlp_kernels.h"
 #include "optimize_kernels.h"
-#include "optimize_mfma_kernel.h"
+#include "optimize_mfma.h"
 #include "optimize_pair_kernel.h"
 #include "seeding.h"
 
@@ -55,36 +55,6 @@ template <typename T, int F, int K>
 void launch_reset(const void *args, int grid, size_t, hipStream_t stream) {
     hipLaunchKernelGGL((ce::optimize_reset_kernel<T, F, K>), dim3(grid), dim3(ce::kBlock), 0,
                        stream, *static_cast<const ce::StepArgs<T> *>(args));
-}
-
-// Any (F <= 64, K <= 16) shape on the f64 matrix cores (optimize_mfma_kernel.h).
-template <int FT>
-void launch_gen(const void *args, int, size_t lds, hipStream_t stream) {
-    const auto &a = *static_cast<const ce::StepArgs<double> *>(args);
-    const int grid = (a.E + ce::kGenWaves - 1) / ce::kGenWaves;
-    hipLaunchKernelGGL((ce::optimize_mfma_kernel<FT>), dim3(grid), dim3(ce::kGenBlock), lds,
-                       stream, a);
-}
-
-void launch_gen_reset(const void *args, int, size_t, hipStream_t stream) {
-    const auto &a = *static_cast<const ce::StepArgs<double> *>(args);
-    const int grid = (a.E + ce::kGenResetWaves - 1) / ce::kGenResetWaves;
-    hipLaunchKernelGGL(ce::optimize_reset_rt_kernel, dim3(grid),
-                       dim3(ce::kWave * ce::kGenResetWaves), 0, stream, a);
-}
-
-const StepFn kGenSteps[ce::kGenMaxFT] = {launch_gen<1>, launch_gen<2>, launch_gen<3>,
-                                         launch_gen<4>};
-
-int set_gen_lds_limits() {
-    const void *fns[ce::kGenMaxFT] = {reinterpret_cast<const void *>(ce::optimize_mfma_kernel<1>),
-                                      reinterpret_cast<const void *>(ce::optimize_mfma_kernel<2>),
-                                      reinterpret_cast<const void *>(ce::optimize_mfma_kernel<3>),
-                                      reinterpret_cast<const void *>(ce::optimize_mfma_kernel<4>)};
-    for (int t = 0; t < ce::kGenMaxFT; ++t)
-        CE_HIP(hipFuncSetAttribute(fns[t], hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   static_cast<int>(2 * ce::gen_block_bytes(t + 1))));
-    return CE_OK;
 }
 
 struct KernelEntry {
@@ -245,9 +215,9 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
     if (e->gen_ft) {
         auto a = make_args<double>(e, act, o);
         if (reset)
-            launch_gen_reset(&a, 0, 0, stream);
+            ce::gen_launch_reset(a, stream);
         else
-            kGenSteps[e->gen_ft - 1](&a, 0, 2 * ce::gen_block_bytes(e->gen_ft), stream);
+            ce::gen_launch_step(a, stream);
         return;
     }
     StepFn fn = reset ? e->kern->reset
@@ -389,8 +359,8 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         if (!(force && force[0] == '1'))
             kern = find_kernel(cfg->precision, cfg->n_features, cfg->n_classes);
         if (!kern) {
-            if (cfg->precision != CE_F64 || cfg->n_features > 16 * ce::kGenMaxFT ||
-                cfg->n_classes > ce::kGenMaxK)
+            if (cfg->precision != CE_F64 || cfg->n_features > ce::kGenMaxF ||
+                cfg->n_classes > ce::kGenMaxClasses)
                 return fail(CE_EUNSUPPORTED,
                             "ce_create: no kernel for F=" + std::to_string(cfg->n_features) +
                                 " K=" + std::to_string(cfg->n_classes) +
@@ -446,10 +416,10 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         CE_TRY(hipMalloc(&e->Xs, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
     } else if (!kern) {
-        e->gen_ft = ce::gen_ft(cfg->n_features);
-        CE_TRY(hipMalloc(&e->X, static_cast<size_t>(ce::gen_rows_padded(cfg->n_rows)) *
-                                    ce::gen_stride(e->gen_ft) * sizeof(double)));
-        if (set_gen_lds_limits() != CE_OK) return bail(CE_EHIP);
+        e->gen_ft = (cfg->n_features + 15) / 16;
+        CE_TRY(hipMalloc(&e->X, static_cast<size_t>(ce::gen_rows_padded_of(cfg->n_rows)) *
+                                    ce::gen_stride_of(cfg->n_features) * sizeof(double)));
+        if (ce::gen_set_lds_limits() != CE_OK) return bail(CE_EHIP);
     } else {
         CE_TRY(hipMalloc(&e->X, ce::stage_bytes_total(cfg->n_features, cfg->n_rows,
                                                       static_cast<int>(e->tsize))));
@@ -509,8 +479,8 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     if (e->gen_ft) {
         // [Npad][RS] float64: F features, zeros to 16 FT + 1, the label as a
         // double in the last column; rows N..Npad-1 are zeros with label -1
-        const int RS = ce::gen_stride(e->gen_ft);
-        const size_t npad = ce::gen_rows_padded(cfg->n_rows);
+        const int RS = ce::gen_stride_of(cfg->n_features);
+        const size_t npad = ce::gen_rows_padded_of(cfg->n_rows);
         std::vector<double> img(npad * RS, 0.0);
         for (size_t r = 0; r < npad; ++r) {
             if (r < N)
@@ -520,7 +490,8 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         if (hipMemcpy(e->X, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice) !=
             hipSuccess)
             return bail(fail(CE_EHIP, "ce_create: dataset upload failed"));
-        e->kernel_name = "optimize_mfma_kernel<" + std::to_string(e->gen_ft) + ">";
+        e->kernel_name =
+            "optimize_mfma_kernel<" + std::to_string((cfg->n_features + 3) / 4) + ">";
     } else if (!mlp) {
     // [rows | labels]: row-major rows padded to ce::row_stride elements (zeros
     // in the pad), then the int32 labels, in one buffer staged with one copy.

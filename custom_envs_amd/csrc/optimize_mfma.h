@@ -1,0 +1,22 @@
+// Host entry points of the runtime-shape f64 MFMA Optimize-v0 kernel
+// (optimize_mfma.hip; the kernel itself is optimize_mfma_kernel.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "optimize_kernels.h"
+
+namespace ce {
+
+constexpr int kGenMaxF = 64;     // F <= 64: 4 feature tiles of 16
+constexpr int kGenMaxClasses = 16;
+
+// Bytes of one [Npad][RS] float64 dataset image row and the padded row count.
+int gen_stride_of(int n_features);
+int gen_rows_padded_of(int n_rows);
+// Raise the dynamic-LDS limit of every instance (double-buffered row blocks).
+int gen_set_lds_limits();
+void gen_launch_step(const StepArgs<double> &a, hipStream_t stream);
+void gen_launch_reset(const StepArgs<double> &a, hipStream_t stream);
+
+}  // namespace ce

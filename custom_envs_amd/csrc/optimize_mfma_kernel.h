@@ -15,25 +15,26 @@
 // streams through LDS in blocks of 64 rows (LDS-DMA, double-buffered), so
 // one HBM/L2 read of a block serves the workgroup's 8 envs.  Per 16-row
 // sub-block and env:
-//   forward   Z (16 rows x 16 classes) = X (16 x 4nk) . W' (4nk x 16):
-//             nk = ceil(F/4) MFMAs; A = X[row l&15][4k + l>>4] from LDS,
-//             B = W'[4k + l>>4][l&15] held in registers for the whole step.
-//   softmax   f64 MFMA C layout: lane l holds class l&15 of rows
-//             (l>>4) + 4r, r = 0..3, so a row's classes are one 16-lane DPP
-//             row: max / sum / first-argmax are 4 xor-shuffle levels each.
+//   forward   Z^T (16 classes x 16 rows) = W'^T (16 x 4nk) . X^T (4nk x 16):
+//             nk = ceil(F/4) MFMAs; A = W'[4k + l>>4][l&15], held in
+//             registers for the whole step, B = X[row l&15][4k + l>>4] from
+//             LDS.
+//   softmax   f64 MFMA C layout: lane l holds row l&15, classes (l>>4) + 4q,
+//             q = 0..3: a row's 16 classes are 4 registers of 4 lanes
+//             (l, l^16, l^32, l^48), so max / sum / first-argmax are an
+//             in-register step plus two permlane-swap levels.
 //   gradient  G (16 features x 16 classes) += X^T (16 x 4 rows) . D (4 rows
-//             x 16 classes) per feature tile: D = P - Y straight from the
-//             softmax registers -- C register r of lane l is row 4r + (l>>4),
-//             class l&15, exactly the B operand of k-step r -- and
-//             A = X[row 4r + (l>>4)][16 ft + (l&15)] from LDS: 4 * ceil(F/16)
-//             MFMAs, no cross-lane reduction (the row sum is the MFMA's k).
+//             x 16 classes) per feature tile, D = P - Y transposed through a
+//             2 KB per-wave LDS tile: A = X[row 4r + (l>>4)][16 ft + (l&15)],
+//             B = D[row 4r + (l>>4)][class l&15]; 4 * ceil(F/16) MFMAs, no
+//             cross-lane reduction (the row sum is the MFMA's k).
 // Minibatches (B < N) gather their B rows per env through the env's row
 // order straight from HBM/L2; the full-data info pass (optimize.py:94-97)
 // is then the LDS stream without the gradient.  With B == N the reference
 // computes the same numbers twice; they are reused.
 // Cross-entropy is -log(p_y + 1e-16) per row (utils_math.py:25-34), taken
-// as -log of per-lane products folded before they can underflow; the
-// argmax is np.argmax's first maximum of P.
+// as -log of per-lane products folded once per block; the argmax is
+// np.argmax's first maximum of P.
 #pragma once
 
 #include "optimize_kernels.h"
@@ -46,6 +47,7 @@ constexpr int kGenWaves = 8;                   // envs per workgroup, one wave e
 constexpr int kGenBlock = kWave * kGenWaves;
 constexpr int kGenRows = 64;                   // dataset rows per LDS block
 constexpr int kGenMaxFT = 4;                   // feature tiles of 16: F <= 64
+constexpr int kGenMaxNK = 16;                  // forward k-steps of 4 features
 constexpr int kGenMaxK = 16;                   // classes: one 16-wide tile
 constexpr int kGenResetWaves = 16;
 
@@ -57,51 +59,110 @@ __host__ __device__ constexpr int gen_stride(int ft) { return 16 * ft + 2; }
 __host__ __device__ constexpr size_t gen_block_bytes(int ft) {
     return static_cast<size_t>(kGenRows) * gen_stride(ft) * sizeof(double);
 }
+__host__ __device__ constexpr size_t gen_lds_bytes(int ft) {
+    return 2 * gen_block_bytes(ft) + kGenWaves * 16 * 17 * sizeof(double);
+}
 __host__ __device__ constexpr int gen_rows_padded(int N) {
     return (N + kGenRows - 1) / kGenRows * kGenRows;
 }
 
-// 16-lane (one DPP row) reductions: xor 1, 2, 4, 8.
-__device__ __forceinline__ double row_max16(double v) {
-    v = fmax(v, xchg<1>(v));
-    v = fmax(v, xchg<2>(v));
-    v = fmax(v, xchg<4>(v));
-    return fmax(v, xchg<8>(v));
+// max / min / sum with the lane l ^ OFF (OFF = 16, 32): one permlane swap
+// per 32-bit half leaves {own, partner} in the two registers.
+template <int OFF>
+__device__ __forceinline__ double lane_max(double v) {
+    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+    unsigned lo = static_cast<unsigned>(b), hi = static_cast<unsigned>(b >> 32);
+    unsigned lo2 = lo, hi2 = hi;
+    swap_halves_u32<OFF>(lo, lo2);
+    swap_halves_u32<OFF>(hi, hi2);
+    const double x = __longlong_as_double(static_cast<long long>(
+        (static_cast<unsigned long long>(hi) << 32) | lo));
+    const double y = __longlong_as_double(static_cast<long long>(
+        (static_cast<unsigned long long>(hi2) << 32) | lo2));
+    return fmax(x, y);
 }
-__device__ __forceinline__ double row_min16(double v) {
-    v = fmin(v, xchg<1>(v));
-    v = fmin(v, xchg<2>(v));
-    v = fmin(v, xchg<4>(v));
-    return fmin(v, xchg<8>(v));
+template <int OFF>
+__device__ __forceinline__ int lane_min(int v) {
+    unsigned a = static_cast<unsigned>(v), b = a;
+    swap_halves_u32<OFF>(a, b);
+    return min(static_cast<int>(a), static_cast<int>(b));
 }
-__device__ __forceinline__ double row_sum16(double v) { return lane_sum<double, 8>(v); }
 
-// One (row, class) entry of the softmax classifier (utils_math.py:51-63,
-// 25-34 and the A7 model): returns P - Y for the gradient (0 for padded
-// rows / classes) and adds the row's cross-entropy factor and argmax hit on
-// the lane holding the row's label.
-__device__ __forceinline__ double gen_softmax(double z, int c, int K, int y, double &prod,
-                                              int &hits) {
-    const bool cls = c < K;
+// The softmax classifier on one row (utils_math.py:51-63, 25-34 and the A7
+// model), spread over 4 lanes x 4 registers: z[q] is class h + 4q of the
+// row.  Writes P - Y to d[q] (0 for padded rows / classes), multiplies the
+// row's cross-entropy factor p_y + 1e-16 into `prod` and adds the argmax
+// hit, both on the lane holding the label class.
+//   argmax(P), first maximum (np.argmax): the row-max logit's classes have
+//   ex = exp_neg(0) = 1 exactly, so their p = 1/s is the maximum of P;
+//   another class's p can only equal it when its ex rounds within 2 ulp of
+//   1, checked exactly in a wave-uniform branch that practically never
+//   runs.  The first such class is a min over the row's 4 lanes.
+__device__ __forceinline__ void gen_softmax(const gen_d4 &z, int h, int K, int y, double (&d)[4],
+                                            double &prod, int &hits) {
     const bool valid = y >= 0;
-    const double m = row_max16(cls ? z : -INFINITY);
-    const double ex = cls ? exp_neg(m - z, MathConsts<double>()) : 0.0;   // exp(z - max)
-    const double s = row_sum16(ex);
-    const double p = ex / s;
-    const double pm = row_max16(cls ? p : -1.0);
-    const double first = row_min16((cls && p == pm) ? static_cast<double>(c) : 99.0);
-    const bool own = valid && c == y;
-    hits += (own && first == static_cast<double>(y)) ? 1 : 0;
-    prod *= own ? p + 1e-16 : 1.0;
-    return (valid && cls) ? p - (c == y ? 1.0 : 0.0) : 0.0;
+    bool cls[4];
+    double m = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        cls[q] = h + 4 * q < K;
+        m = cls[q] ? fmax(m, z[q]) : m;
+    }
+    m = lane_max<32>(lane_max<16>(m));
+    double ex[4], s = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        ex[q] = cls[q] ? exp_neg(m - z[q], MathConsts<double>()) : 0.0;   // exp(z - max)
+        s += ex[q];
+    }
+    s = fold_pair<16>(s, s);                     // + lane l^16, then l^32: the row's 4 lanes
+    s = fold_pair<32>(s, s);
+    const double inv = 1.0 / s;
+    int first = 99;
+    bool near = false;
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+        first = (cls[q] && ex[q] == 1.0) ? h + 4 * q : first;
+        near = near || (cls[q] && ex[q] < 1.0 && ex[q] > 1.0 - 4.5e-16);
+    }
+    if (__any(near)) {
+#pragma unroll
+        for (int q = 3; q >= 0; --q)
+            first = (cls[q] && (ex[q] == 1.0 || ex[q] / s == 1.0 / s)) ? h + 4 * q : first;
+    }
+    first = lane_min<32>(lane_min<16>(first));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double p = ex[q] * inv;
+        const bool own = valid && h + 4 * q == y;
+        hits += (own && first == y) ? 1 : 0;
+        prod *= own ? p + 1e-16 : 1.0;
+        d[q] = (valid && cls[q]) ? p - (own ? 1.0 : 0.0) : 0.0;
+    }
 }
 
+// -log of a lane's product of cross-entropy factors, folded once per LDS
+// block: at most 16 factors per lane per block, each in (1e-16, 1], so the
+// product stays above 1e-256 (no underflow, no branch).
 __device__ __forceinline__ void gen_fold(double &loss, double &prod) {
-    // factors are in (1e-16, 1]: fold long before the product can underflow
-    if (__any(prod < 1e-200)) {
-        loss -= log_pos(prod);
-        prod = 1.0;
-    }
+    loss -= log_pos(prod);
+    prod = 1.0;
+}
+
+// Per-wave 16 x 16 tile that turns D from the softmax layout (lane = row)
+// into the gradient's B operand layout (lane = class): row stride 17
+// doubles keeps the 8-byte stores and loads conflict-free.
+constexpr int kGenDStride = 17;
+constexpr size_t kGenDBytes = 16 * kGenDStride * sizeof(double);
+
+__device__ __forceinline__ void gen_grad(const double (&d)[4], double *dsh, int c, int h,
+                                         double (&bd)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dsh[c * kGenDStride + h + 4 * q] = d[q];   // row c, class h + 4q
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bd[r] = dsh[(4 * r + h) * kGenDStride + c];  // row 4r + h, class c
+    __builtin_amdgcn_wave_barrier();
 }
 
 // W <- W0, histories <- 0, current_step <- 0, order <- order[perm]
@@ -138,10 +199,13 @@ __global__ __launch_bounds__(kWave *kGenResetWaves) void optimize_reset_rt_kerne
     for (int i = lane; i < 2 * P + 1; i += kWave) obs[i] = 0.0f;
 }
 
-template <int FT>
+// NK = ceil(F / 4) forward k-steps (a compile-time count, so the MFMA
+// chains are straight-line code with their LDS reads issued together),
+// FT = ceil(F / 16) gradient feature tiles.
+template <int NK>
 __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<double> a) {
+    constexpr int FT = (NK + 3) / 4;
     constexpr int RS = gen_stride(FT);
-    constexpr int NK = 4 * FT;                       // forward k-steps at most
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -149,12 +213,12 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
     const bool active = e < a.E;                     // wave-uniform
     const int eidx = active ? e : 0;
     const int F = a.F, K = a.K, P = F * K, N = a.N, B = a.B;
-    const int nk = (F + 3) >> 2;
     const int c = lane & 15, h = lane >> 4;
     const double *X = reinterpret_cast<const double *>(a.data);
     const size_t pbase = static_cast<size_t>(eidx) * P;
+    double *dsh = reinterpret_cast<double *>(smem + 2 * gen_block_bytes(FT) + wave * kGenDBytes);
 
-    // ---- state: W' = W - a (optimize.py:74-75) as the forward's B operands
+    // ---- state: W' = W - a (optimize.py:74-75) as the forward's A operands
     const int step_prev = a.step[eidx];
     const double lprev = a.L[eidx];
     double wb[NK];
@@ -182,31 +246,28 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
         const int32_t *order = a.order + sel * static_cast<size_t>(a.E) * N +
                                static_cast<size_t>(e) * N;
         for (int i0 = 0; i0 < B; i0 += 16) {
-            const int ia = i0 + c;
-            const double *xa = X + static_cast<size_t>(ia < B ? order[ia] : 0) * RS;
-            const bool va = ia < B;
+            const int ia = i0 + c;                           // this lane's row of Z^T
+            const double *xa = X + static_cast<size_t>(order[ia < B ? ia : 0]) * RS;
+            double av[NK];
+#pragma unroll
+            for (int k = 0; k < NK; ++k) av[k] = ia < B ? xa[4 * k + h] : 0.0;
+            const int y = ia < B ? static_cast<int>(xa[RS - 1]) : -1;
             gen_d4 z = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int k = 0; k < NK; ++k)
-                if (k < nk)
-                    z = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? xa[4 * k + h] : 0.0, wb[k], z,
-                                                             0, 0, 0);
-            const double *xr[4];
-            double d[4];
+            for (int k = 0; k < NK; ++k) z = __builtin_amdgcn_mfma_f64_16x16x4f64(wb[k], av[k], z, 0, 0, 0);
+            double d[4], bd[4];
+            gen_softmax(z, h, K, y, d, prod, hits);
+            gen_grad(d, dsh, c, h, bd);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int ir = i0 + h + 4 * r;
-                xr[r] = X + static_cast<size_t>(ir < B ? order[ir] : 0) * RS;
-                const int y = ir < B ? static_cast<int>(xr[r][RS - 1]) : -1;
-                d[r] = gen_softmax(z[r], c, K, y, prod, hits);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
+                const int ir = i0 + 4 * r + h;
+                const double *xr = X + static_cast<size_t>(order[ir < B ? ir : 0]) * RS;
 #pragma unroll
                 for (int t = 0; t < FT; ++t)
-                    g[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[r][16 * t + c], d[r], g[t], 0,
-                                                                0, 0);
-            gen_fold(loss, prod);
+                    g[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ir < B ? xr[16 * t + c] : 0.0, bd[r],
+                                                                g[t], 0, 0, 0);
+            }
+            if ((i0 & 48) == 48) gen_fold(loss, prod);
         }
     }
 
@@ -237,33 +298,33 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
 #pragma unroll 1
             for (int sb = 0; sb < kGenRows / 16; ++sb) {
                 const double *xs = xb + sb * 16 * RS;
+                double av[NK];
+#pragma unroll
+                for (int k = 0; k < NK; ++k) av[k] = xs[c * RS + 4 * k + h];
+                const int y = static_cast<int>(xs[c * RS + RS - 1]);
                 gen_d4 z = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                 for (int k = 0; k < NK; ++k)
-                    if (k < nk)
-                        z = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[c * RS + 4 * k + h], wb[k], z,
-                                                                 0, 0, 0);
+                    z = __builtin_amdgcn_mfma_f64_16x16x4f64(wb[k], av[k], z, 0, 0, 0);
                 double d[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int y = static_cast<int>(xs[(h + 4 * r) * RS + RS - 1]);
-                    if (full)
-                        d[r] = gen_softmax(z[r], c, K, y, prod, hits);
-                    else
-                        d[r] = gen_softmax(z[r], c, K, y, fprod, fhits);
-                }
                 if (full) {
+                    double bd[4];
+                    gen_softmax(z, h, K, y, d, prod, hits);
+                    gen_grad(d, dsh, c, h, bd);
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
 #pragma unroll
                         for (int t = 0; t < FT; ++t)
                             g[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                                xs[(h + 4 * r) * RS + 16 * t + c], d[r], g[t], 0, 0, 0);
-                    gen_fold(loss, prod);
+                                xs[(4 * r + h) * RS + 16 * t + c], bd[r], g[t], 0, 0, 0);
                 } else {
-                    gen_fold(floss, fprod);
+                    gen_softmax(z, h, K, y, d, fprod, fhits);
                 }
             }
+            if (full)
+                gen_fold(loss, prod);
+            else
+                gen_fold(floss, fprod);
         }
     }
     if (!active) return;
@@ -303,7 +364,7 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             const int f = 4 * k + h;
-            if (k < nk && f < F && c < K) a.W[pbase + f * K + c] = wb[k];
+            if (f < F && c < K) a.W[pbase + f * K + c] = wb[k];
         }
     }
     for (int i = lane; i < P; i += kWave) obs[i] = 0.0f;   // wght_hist is identically 0

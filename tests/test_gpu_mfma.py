@@ -81,7 +81,7 @@ def test_mnist_idx_fixture_through_make():
     from custom_envs_amd.data import load_data
     data_dir = os.path.join(GOLDEN, 'idx')
     env = make('Optimize-v0', data_set='mnist', data_dir=data_dir)
-    assert env.engine.step_kernel == 'optimize_mfma_kernel<4>'
+    assert env.engine.step_kernel == 'optimize_mfma_kernel<13>'   # NK = ceil(49 / 4)
     assert env.observation_space.shape == (2 * 490 + 1,) and env.action_space.shape == (490,)
     seq = load_data('mnist', batch_size=None, data_dir=data_dir)
     ref = OracleEnv(seq.features, seq.targets)
@@ -107,7 +107,7 @@ def test_image_shape_many_envs(batch_size):
     (one full and one partial workgroup), 43 steps across an auto-reset."""
     ds = _classes(1000, 49, 10, 1)
     eng = _engine(ds, 13, batch_size)
-    assert eng.step_kernel == 'optimize_mfma_kernel<4>'
+    assert eng.step_kernel == 'optimize_mfma_kernel<13>'
     _check(ds, batch_size, eng, [0, 7, 8, 12], 43)
     eng.close()
 
@@ -117,7 +117,7 @@ def test_every_feature_tile_count(shape):
     F, K = shape
     ds = _classes(300, F, K, F + K)
     eng = _engine(ds, 9, None, generic=True)
-    assert eng.step_kernel == 'optimize_mfma_kernel<%d>' % ((F + 15) // 16)
+    assert eng.step_kernel == 'optimize_mfma_kernel<%d>' % ((F + 3) // 4)
     _check(ds, None, eng, [0, 8], 41)
     eng.close()
 
@@ -127,7 +127,7 @@ def test_register_shapes_forced_generic(lr_dataset, batch_size):
     """The benchmark shape (256 x 10, K = 2) on the MFMA kernel agrees with
     the oracle as the register kernels do."""
     eng = _engine(lr_dataset, 10, batch_size, generic=True)
-    assert eng.step_kernel == 'optimize_mfma_kernel<1>'
+    assert eng.step_kernel == 'optimize_mfma_kernel<3>'
     _check(lr_dataset, batch_size, eng, [0, 9], 42)
     eng.close()
 
