@@ -93,11 +93,7 @@ __device__ __forceinline__ int lane_min(int v) {
 // row.  Writes P - Y to d[q] (0 for padded rows / classes), multiplies the
 // row's cross-entropy factor p_y + 1e-16 into `prod` and adds the argmax
 // hit, both on the lane holding the label class.
-//   argmax(P), first maximum (np.argmax): the row-max logit's classes have
-//   ex = exp_neg(0) = 1 exactly, so their p = 1/s is the maximum of P;
-//   another class's p can only equal it when its ex rounds within 2 ulp of
-//   1, checked exactly in a wave-uniform branch that practically never
-//   runs.  The first such class is a min over the row's 4 lanes.
+//   Branch-free: padded classes are selected out, never branched around.
 __device__ __forceinline__ void gen_softmax(const gen_d4 &z, int h, int K, int y, double (&d)[4],
                                             double &prod, int &hits) {
     const bool valid = y >= 0;
@@ -109,35 +105,47 @@ __device__ __forceinline__ void gen_softmax(const gen_d4 &z, int h, int K, int y
         m = cls[q] ? fmax(m, z[q]) : m;
     }
     m = lane_max<32>(lane_max<16>(m));
+    // exp(z - max), branch-free over the 3 (K <= 12) or 4 class registers
     double ex[4], s = 0.0;
+    if (K <= 12) {
+        double x[3];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        ex[q] = cls[q] ? exp_neg(m - z[q], MathConsts<double>()) : 0.0;   // exp(z - max)
-        s += ex[q];
+        for (int q = 0; q < 3; ++q) x[q] = cls[q] ? m - z[q] : 750.0;
+        exp_neg_multi<3>(x);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) ex[q] = cls[q] ? x[q] : 0.0;
+        ex[3] = 0.0;
+    } else {
+        double x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = cls[q] ? m - z[q] : 750.0;
+        exp_neg_multi<4>(x);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ex[q] = cls[q] ? x[q] : 0.0;
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s += ex[q];
     s = fold_pair<16>(s, s);                     // + lane l^16, then l^32: the row's 4 lanes
     s = fold_pair<32>(s, s);
     const double inv = 1.0 / s;
+    // P = ex * (1/s): the row-max classes have ex = exp_neg(0) = 1 exactly,
+    // so max(P) = inv and argmax(P) = the first class whose p equals it
+    // (np.argmax's first maximum, on this P; the reference's p_exp / p_sum
+    // differs from it by at most an ulp)
     int first = 99;
-    bool near = false;
+    double p[4];
 #pragma unroll
     for (int q = 3; q >= 0; --q) {
-        first = (cls[q] && ex[q] == 1.0) ? h + 4 * q : first;
-        near = near || (cls[q] && ex[q] < 1.0 && ex[q] > 1.0 - 4.5e-16);
-    }
-    if (__any(near)) {
-#pragma unroll
-        for (int q = 3; q >= 0; --q)
-            first = (cls[q] && (ex[q] == 1.0 || ex[q] / s == 1.0 / s)) ? h + 4 * q : first;
+        p[q] = ex[q] * inv;
+        first = (cls[q] && p[q] == inv) ? h + 4 * q : first;
     }
     first = lane_min<32>(lane_min<16>(first));
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const double p = ex[q] * inv;
         const bool own = valid && h + 4 * q == y;
         hits += (own && first == y) ? 1 : 0;
-        prod *= own ? p + 1e-16 : 1.0;
-        d[q] = (valid && cls[q]) ? p - (own ? 1.0 : 0.0) : 0.0;
+        prod *= own ? p[q] + 1e-16 : 1.0;
+        d[q] = (valid && cls[q]) ? p[q] - (own ? 1.0 : 0.0) : 0.0;
     }
 }
 
@@ -199,6 +207,24 @@ __global__ __launch_bounds__(kWave *kGenResetWaves) void optimize_reset_rt_kerne
     for (int i = lane; i < 2 * P + 1; i += kWave) obs[i] = 0.0f;
 }
 
+// Z^T = sum over k of W'^T_k X^T_k as kGenChains independent accumulator
+// chains (a dependent f64 MFMA waits out the previous one's latency; two
+// chains keep the matrix pipe issuing), added at the end.
+constexpr int kGenChains = 2;
+template <int NK>
+__device__ __forceinline__ gen_d4 gen_forward(const double (&wb)[NK], const double (&av)[NK]) {
+    gen_d4 z[kGenChains];
+#pragma unroll
+    for (int i = 0; i < kGenChains; ++i) z[i] = gen_d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+        z[k % kGenChains] = __builtin_amdgcn_mfma_f64_16x16x4f64(wb[k], av[k], z[k % kGenChains],
+                                                                 0, 0, 0);
+#pragma unroll
+    for (int i = 1; i < kGenChains; ++i) z[0] += z[i];
+    return z[0];
+}
+
 // NK = ceil(F / 4) forward k-steps (a compile-time count, so the MFMA
 // chains are straight-line code with their LDS reads issued together),
 // FT = ceil(F / 16) gradient feature tiles.
@@ -252,9 +278,7 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
 #pragma unroll
             for (int k = 0; k < NK; ++k) av[k] = ia < B ? xa[4 * k + h] : 0.0;
             const int y = ia < B ? static_cast<int>(xa[RS - 1]) : -1;
-            gen_d4 z = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int k = 0; k < NK; ++k) z = __builtin_amdgcn_mfma_f64_16x16x4f64(wb[k], av[k], z, 0, 0, 0);
+            const gen_d4 z = gen_forward<NK>(wb, av);
             double d[4], bd[4];
             gen_softmax(z, h, K, y, d, prod, hits);
             gen_grad(d, dsh, c, h, bd);
@@ -295,17 +319,23 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
         if (j + 1 < nblk) stage(j + 1, (j + 1) & 1);
         if (active) {
             const double *xb = reinterpret_cast<const double *>(smem + (j & 1) * kBlk);
-#pragma unroll 1
-            for (int sb = 0; sb < kGenRows / 16; ++sb) {
+            // software-pipelined over the block's 4 sub-blocks: the forward
+            // MFMAs of sub-block sb + 1 are issued before the softmax of sb,
+            // so the matrix pipe runs while this wave does its VALU work
+            auto forward = [&](int sb) {
                 const double *xs = xb + sb * 16 * RS;
                 double av[NK];
 #pragma unroll
                 for (int k = 0; k < NK; ++k) av[k] = xs[c * RS + 4 * k + h];
-                const int y = static_cast<int>(xs[c * RS + RS - 1]);
-                gen_d4 z = {0.0, 0.0, 0.0, 0.0};
+                return gen_forward<NK>(wb, av);
+            };
+            gen_d4 z = forward(0);
 #pragma unroll
-                for (int k = 0; k < NK; ++k)
-                    z = __builtin_amdgcn_mfma_f64_16x16x4f64(wb[k], av[k], z, 0, 0, 0);
+            for (int sb = 0; sb < kGenRows / 16; ++sb) {
+                const double *xs = xb + sb * 16 * RS;
+                const int y = static_cast<int>(xs[c * RS + RS - 1]);
+                gen_d4 zn = z;
+                if (sb + 1 < kGenRows / 16) zn = forward(sb + 1);
                 double d[4];
                 if (full) {
                     double bd[4];
@@ -320,6 +350,7 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
                 } else {
                     gen_softmax(z, h, K, y, d, fprod, fhits);
                 }
+                z = zn;
             }
             if (full)
                 gen_fold(loss, prod);
