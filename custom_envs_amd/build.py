@@ -34,7 +34,7 @@ def sources():
 
 def headers():
     return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'optimize_pair_kernel.h',
-                                            'optimize_mfma_kernel.h', 'optimize_mfma.h',
+                                            'optimize_mfma_kernel.h', 'optimize_mfma.h', 'optimize_lr_mfma.h',
                                             'multiopt_kernels.h', 'mlp_kernels.h', 'multinn_kernels.h', 'common.h', 'seeding.h')] + [
         os.path.join(ROOT, 'include', 'custom_envs_amd.h')]
 

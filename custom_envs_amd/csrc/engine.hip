@@ -116,6 +116,7 @@ struct ce_engine {
     bool staged = false;      // dataset fits the per-block LDS stage
     StepFn pair = nullptr;    // two-envs-per-wave step kernel, when the shape has one
     int gen_ft = 0;           // > 0: the runtime-shape MFMA kernel with this many feature tiles
+    bool lr_mfma = false;     // two-class full-batch MFMA kernel (optimize_lr_mfma.h)
     std::string kernel_name;  // what ce_step_kernel reports
     size_t stage_bytes = 0;
     ce::GraphCache graphs;   // ce_step_many
@@ -210,6 +211,14 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
             if (e->mlp_phases & 1) hipLaunchKernelGGL(ce::mlp_train_kernel, grid, block, 0, stream, a);
             if (e->mlp_phases & 2) hipLaunchKernelGGL(ce::mlp_info_kernel, grid, block, 0, stream, a);
         }
+        return;
+    }
+    if (e->lr_mfma) {
+        auto a = make_args<double>(e, act, o);
+        if (reset)
+            ce::gen_launch_reset(a, stream);
+        else
+            ce::lr_launch_step(a, stream);
         return;
     }
     if (e->gen_ft) {
@@ -342,6 +351,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     if (cfg->max_steps <= 0) return fail(CE_EINVAL, "ce_create: max_steps must be positive");
     const bool mlp = cfg->problem == CE_PROBLEM_MLP;
     const KernelEntry *kern = nullptr;
+    bool lr_path = false;
     if (mlp) {
         // the shapes mlp_kernels.h is written for (config 3: 784 -> 64 -> 10, B = 32)
         if (cfg->precision != CE_F32)
@@ -356,9 +366,17 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         // a register-path instance when the shape has one (unless CE_GENERIC=1
         // forces the runtime-shape kernel, for tests), else the MFMA kernel
         const char *force = std::getenv("CE_GENERIC");
-        if (!(force && force[0] == '1'))
+        const bool generic = force && force[0] == '1';
+        // the two-class full-batch shapes (the benchmark) run on the MFMA
+        // kernel with envs along N, unless CE_LR_MFMA=0 or a CE_PAIR_U
+        // override asks for the register kernels
+        const char *lrm = std::getenv("CE_LR_MFMA");
+        lr_path = !generic && !(lrm && lrm[0] == '0') && !std::getenv("CE_PAIR_U") &&
+                  cfg->precision == CE_F64 && cfg->batch_size == cfg->n_rows &&
+                  ce::lr_shape_ok(cfg->n_features, cfg->n_classes);
+        if (!generic && !lr_path)
             kern = find_kernel(cfg->precision, cfg->n_features, cfg->n_classes);
-        if (!kern) {
+        if (!kern && !lr_path) {
             if (cfg->precision != CE_F64 || cfg->n_features > ce::kGenMaxF ||
                 cfg->n_classes > ce::kGenMaxClasses)
                 return fail(CE_EUNSUPPORTED,
@@ -415,6 +433,10 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         CE_TRY(hipMalloc(&e->X, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->Xs, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
+    } else if (lr_path) {
+        e->lr_mfma = true;
+        CE_TRY(hipMalloc(&e->X, ce::lr_image_doubles(cfg->n_features, cfg->n_rows) *
+                                    sizeof(double)));
     } else if (!kern) {
         e->gen_ft = (cfg->n_features + 15) / 16;
         CE_TRY(hipMalloc(&e->X, static_cast<size_t>(ce::gen_rows_padded_of(cfg->n_rows)) *
@@ -476,7 +498,15 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         CE_TRY(hipMemcpy(e->label, labels, N * sizeof(int32_t), hipMemcpyHostToDevice));
     }
 #undef CE_TRY
-    if (e->gen_ft) {
+    if (e->lr_mfma) {
+        std::vector<double> img(ce::lr_image_doubles(cfg->n_features, cfg->n_rows));
+        ce::lr_build_image(cfg->n_features, cfg->n_rows, features, labels, img.data());
+        if (hipMemcpy(e->X, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice) !=
+            hipSuccess)
+            return bail(fail(CE_EHIP, "ce_create: dataset upload failed"));
+        e->kernel_name = "optimize_lr_mfma_kernel<" +
+                         std::to_string((cfg->n_features + 3) / 4) + ">";
+    } else if (e->gen_ft) {
         // [Npad][RS] float64: F features, zeros to 16 FT + 1, the label as a
         // double in the last column; rows N..Npad-1 are zeros with label -1
         const int RS = ce::gen_stride_of(cfg->n_features);

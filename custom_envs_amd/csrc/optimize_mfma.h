@@ -19,4 +19,13 @@ int gen_set_lds_limits();
 void gen_launch_step(const StepArgs<double> &a, hipStream_t stream);
 void gen_launch_reset(const StepArgs<double> &a, hipStream_t stream);
 
+// Two-class, full-batch, F <= 16 (optimize_lr_mfma.h): 16 envs per workgroup
+// on the MFMA N dimension.  The dataset image is fragment-ordered
+// (lr_build_image); lr_image_doubles gives its size.
+bool lr_shape_ok(int n_features, int n_classes);
+size_t lr_image_doubles(int n_features, int n_rows);
+void lr_build_image(int n_features, int n_rows, const double *features, const int32_t *labels,
+                    double *image);
+void lr_launch_step(const StepArgs<double> &a, hipStream_t stream);
+
 }  // namespace ce

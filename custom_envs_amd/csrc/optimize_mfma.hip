@@ -3,7 +3,10 @@
 #include "optimize_mfma.h"
 
 #include "common.h"
+#include "optimize_lr_mfma.h"
 #include "optimize_mfma_kernel.h"
+
+#include <cstring>
 
 namespace ce {
 
@@ -33,7 +36,46 @@ struct Table {
 using Gen = Table<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
 static_assert(16 == kGenMaxF / 4, "one instance per k-step count");
 
+template <int NKF>
+void launch_lr(const StepArgs<double> &a, hipStream_t stream) {
+    const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
+    hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF>), dim3(grid), dim3(kLrBlock), 0, stream, a);
+}
+constexpr GenFn kLrSteps[4] = {launch_lr<1>, launch_lr<2>, launch_lr<3>, launch_lr<4>};
+
 }  // namespace
+
+bool lr_shape_ok(int n_features, int n_classes) { return lr_mfma_shape(n_features, n_classes); }
+
+size_t lr_image_doubles(int n_features, int n_rows) {
+    return static_cast<size_t>((n_rows + 15) / 16) * lr_tile_doubles(lr_nkf(n_features));
+}
+
+void lr_build_image(int F, int N, const double *x, const int32_t *y, double *img) {
+    const int nkf = lr_nkf(F), TD = lr_tile_doubles(nkf), ntiles = (N + 15) / 16;
+    // sign-folded rows s_y x (s_y = +1 for y = 0, -1 for y = 1): exact
+    auto xt = [&](int r, int f) -> double {
+        if (r >= N || f >= F) return 0.0;
+        return y[r] != 0 ? -x[static_cast<size_t>(r) * F + f] : x[static_cast<size_t>(r) * F + f];
+    };
+    auto label = [&](int r) -> int32_t { return r < N ? y[r] : -1; };
+    for (int t = 0; t < ntiles; ++t) {
+        double *ti = img + static_cast<size_t>(t) * TD;
+        for (int l = 0; l < kWave; ++l) {
+            const int c = l & 15, h = l >> 4;
+            for (int k = 0; k < nkf; ++k) ti[k * kWave + l] = xt(16 * t + c, 4 * k + h);
+            for (int q = 0; q < 4; ++q) ti[(nkf + q) * kWave + l] = xt(16 * t + h + 4 * q, c);
+            int32_t lab[4];
+            for (int q = 0; q < 4; ++q) lab[q] = label(16 * t + h + 4 * q);
+            std::memcpy(&ti[(nkf + 4) * kWave + l], &lab[0], 8);
+            std::memcpy(&ti[(nkf + 5) * kWave + l], &lab[2], 8);
+        }
+    }
+}
+
+void lr_launch_step(const StepArgs<double> &a, hipStream_t stream) {
+    kLrSteps[lr_nkf(a.F) - 1](a, stream);
+}
 
 int gen_stride_of(int n_features) { return gen_stride(gen_ft(n_features)); }
 int gen_rows_padded_of(int n_rows) { return gen_rows_padded(n_rows); }

@@ -176,3 +176,51 @@ def test_unsupported_shapes_fail_loudly():
     ds = _classes(64, 49, 10, 0)
     with pytest.raises(NativeEngineError, match='float64'):
         _engine(ds, 2, precision='f32')
+
+
+# ---------------------------------------------------------------------------
+# The two-class full-batch kernel with envs on the MFMA N dimension
+# (optimize_lr_mfma.h): the default for K = 2, F <= 16, B = N in float64.
+
+def _two_class(n_rows, n_features, seed):
+    rs = np.random.RandomState(seed)
+    x = rs.normal(0, 1.0, (n_rows, n_features))
+    y = (x @ rs.normal(size=n_features) + rs.normal(0, 0.7, n_rows) > 0).astype(int)
+    return x, np.eye(2)[y]
+
+
+@pytest.mark.parametrize('n_rows,n_features,num_envs', [
+    (256, 10, 37), (200, 1, 16), (203, 13, 17), (1000, 16, 5), (4000, 4, 3), (256, 5, 1)])
+def test_lr_mfma_kernel_matches_oracle(n_rows, n_features, num_envs):
+    """Ragged row tiles (N % 16 != 0), partial 16-env groups, every k-step
+    count, many tiles per wave (the cross-entropy product folds)."""
+    ds = _two_class(n_rows, n_features, n_rows + n_features)
+    eng = _engine(ds, num_envs, None)
+    assert eng.step_kernel == 'optimize_lr_mfma_kernel<%d>' % ((n_features + 3) // 4)
+    envs = sorted({0, num_envs // 2, num_envs - 1})
+    _check(ds, None, eng, envs, 43)
+    eng.close()
+
+
+def test_lr_mfma_agrees_with_register_kernel(lr_dataset):
+    """Same envs through the MFMA kernel and the two-envs-per-wave register
+    kernel (CE_LR_MFMA=0): float64 results agree to float32 rounding."""
+    E, T = 64, 45
+    acts = np.random.RandomState(3).normal(0, 0.02, (T, E, 20)).astype(np.float32)
+    outs = []
+    for flag in ('1', '0'):
+        os.environ['CE_LR_MFMA'] = flag
+        try:
+            eng = _engine(lr_dataset, E, None)
+        finally:
+            os.environ.pop('CE_LR_MFMA')
+        assert ('lr_mfma' in eng.step_kernel) == (flag == '1')
+        eng.seed(list(range(E)))
+        eng.reset()
+        outs.append([{k: v.copy() for k, v in eng.step(acts[t]).items()} for t in range(T)])
+        eng.close()
+    for a, b in zip(*outs):
+        np.testing.assert_allclose(a['obs'], b['obs'], rtol=2e-6, atol=1e-9)
+        assert np.array_equal(a['done'], b['done'])
+        assert np.array_equal(a['episode_len'], b['episode_len'])
+        assert np.array_equal(a['accuracy'], b['accuracy'])
