@@ -367,11 +367,12 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         // forces the runtime-shape kernel, for tests), else the MFMA kernel
         const char *force = std::getenv("CE_GENERIC");
         const bool generic = force && force[0] == '1';
-        // the two-class full-batch shapes (the benchmark) run on the MFMA
-        // kernel with envs along N, unless CE_LR_MFMA=0 or a CE_PAIR_U
-        // override asks for the register kernels
+        // CE_LR_MFMA=1: the two-class full-batch shapes run on the MFMA kernel
+        // with envs along N (optimize_lr_mfma.h).  Measured at 4096 envs it
+        // ties the two-envs-per-wave register kernel (6.6-6.7 us vs 6.3-6.7
+        // us per step), which therefore stays the default.
         const char *lrm = std::getenv("CE_LR_MFMA");
-        lr_path = !generic && !(lrm && lrm[0] == '0') && !std::getenv("CE_PAIR_U") &&
+        lr_path = !generic && (lrm && lrm[0] == '1') && !std::getenv("CE_PAIR_U") &&
                   cfg->precision == CE_F64 && cfg->batch_size == cfg->n_rows &&
                   ce::lr_shape_ok(cfg->n_features, cfg->n_classes);
         if (!generic && !lr_path)

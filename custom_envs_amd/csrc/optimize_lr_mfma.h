@@ -36,6 +36,8 @@ constexpr int kLrWaves = 8;                    // waves per workgroup (row split
 constexpr int kLrBlock = kWave * kLrWaves;
 constexpr int kLrMaxF = 16;
 
+static_assert(kLrEnvs * 2 * kLrMaxF <= kLrBlock, "one epilogue thread per (env, parameter)");
+
 __host__ __device__ constexpr bool lr_mfma_shape(int F, int K) { return K == 2 && F <= kLrMaxF; }
 __host__ __device__ constexpr int lr_nkf(int F) { return (F + 3) / 4; }
 // float64 operands per lane per 16-row tile: nkf forward A + 4 gradient A,
@@ -57,6 +59,11 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     __shared__ double tot[6][kWave];                    // workgroup totals
     __shared__ double wsh[kLrEnvs][P_MAX];              // W' of the group's envs
     __shared__ int wipe_sh[kLrEnvs];                    // auto-reset this step
+#ifdef CE_DIAG
+    unsigned long long stamps[kStamps] = {0};
+    stamps[6] = __builtin_amdgcn_s_memrealtime();
+#endif
+    CE_STAMP(0);
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int c = lane & 15, h = lane >> 4;
@@ -85,28 +92,65 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
         }
     }
 
+    // ---- the epilogue's state loads, issued now so their latency hides
+    // under the row work: per (env, parameter) thread G and W0, per env L
+    // and the step counter
+    const int tid = threadIdx.x;
+    const int B = a.B;
+    const int np_ = kLrEnvs * P;
+    double g_prev = 0.0, w_init = 0.0;
+    {
+        const int j = tid / P;
+        const int ee = e0 + (tid < np_ ? j : 0);
+        const size_t gi = static_cast<size_t>(ee < a.E ? ee : 0) * P + (tid < np_ ? tid - j * P : 0);
+        g_prev = a.G[gi];
+        w_init = a.W0[gi];
+    }
+    const int es = e0 + (tid < kLrEnvs ? tid : 0);
+    const double lprev = a.L[es < a.E ? es : 0];
+    const int step_prev = a.step[es < a.E ? es : 0];
+
     lr_d4 s = {0.0, 0.0, 0.0, 0.0};
     double prod = 1.0, nlog = 0.0;
     int hits = 0;
     int since = 0;
+    // the wave's row tiles, each one's operands loaded a tile ahead
+    double xf[NKF], xg[4];
+    int2 y01, y23;
+    auto load_tile = [&](int t) {
+        const double *ti = img + static_cast<size_t>(t) * TD;
+#pragma unroll
+        for (int k = 0; k < NKF; ++k) xf[k] = ti[k * kWave + lane];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xg[q] = ti[(NKF + q) * kWave + lane];
+        y01 = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
+        y23 = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
+    };
+    if (wave < ntiles) load_tile(wave);
+#ifdef CE_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    CE_STAMP(1);
+#if defined(CE_LR_EXP) && (CE_LR_EXP == 1 || CE_LR_EXP == 3)
+    for (int t = ntiles; t < ntiles; t += kLrWaves) {     // experiment: no row work
+#else
     for (int t = wave; t < ntiles; t += kLrWaves) {
+#endif
         if (++since > 4) {                              // 16 factors in (1e-16, 1]: fold
             nlog -= log_pos(prod);
             prod = 1.0;
             since = 1;
         }
-        const double *ti = img + static_cast<size_t>(t) * TD;
-        double xf[NKF], xg[4];
+        double cf[NKF], cg[4];
 #pragma unroll
-        for (int k = 0; k < NKF; ++k) xf[k] = ti[k * kWave + lane];
+        for (int k = 0; k < NKF; ++k) cf[k] = xf[k];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) xg[q] = ti[(NKF + q) * kWave + lane];
-        const int2 y01 = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
-        const int2 y23 = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
+        for (int q = 0; q < 4; ++q) cg[q] = xg[q];
         const int ys[4] = {y01.x, y01.y, y23.x, y23.y};
+        if (t + kLrWaves < ntiles) load_tile(t + kLrWaves);
         lr_d4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < NKF; ++k) u = __builtin_amdgcn_mfma_f64_16x16x4f64(xf[k], wd[k], u, 0, 0, 0);
+        for (int k = 0; k < NKF; ++k) u = __builtin_amdgcn_mfma_f64_16x16x4f64(cf[k], wd[k], u, 0, 0, 0);
         // two-class softmax of TwoClassModel per (row, env): t = e^-|u|,
         // p of the larger logit 1/(1+t); q = 1 - p_y (the gradient weight);
         // a tie (t == 1, p0 == p1) is np.argmax's class 0: hit iff y == 0
@@ -129,7 +173,7 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
             hits += (valid && hit) ? 1 : 0;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s = __builtin_amdgcn_mfma_f64_16x16x4f64(xg[q], qv[q], s, 0, 0, 0);
+        for (int q = 0; q < 4; ++q) s = __builtin_amdgcn_mfma_f64_16x16x4f64(cg[q], qv[q], s, 0, 0, 0);
     }
     // partials of this wave: s (features h + 4r of env c), -log of the
     // cross-entropy factors, hits
@@ -139,6 +183,7 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     red[wave][3][lane] = s[3];
     red[wave][4][lane] = nlog - log_pos(prod);
     red[wave][5][lane] = static_cast<double>(hits);
+    CE_STAMP(2);
     __syncthreads();
     if (wave < 6) {                                     // wave v sums value v over waves
         double acc = 0.0;
@@ -151,18 +196,20 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
         tot[wave][lane] = acc;
     }
     __syncthreads();
+    CE_STAMP(3);
 
     // ---- epilogue over the group's 16 envs, spread over the threads
-    const int tid = threadIdx.x;
-    const int B = a.B;
+#if defined(CE_LR_EXP) && (CE_LR_EXP == 2 || CE_LR_EXP == 3)
+    if (tid < kLrEnvs && e0 + tid < a.E) a.reward[e0 + tid] = static_cast<float>(tot[4][tid]);
+    return;                                             // experiment: no epilogue
+#endif
     // per env scalars: thread j < 16 handles env e0 + j
     const int OBS = 2 * P + 1;
     if (tid < kLrEnvs && e0 + tid < a.E) {
         const int ee = e0 + tid;
         const double loss = tot[4][tid] / B;            // lane tid holds env tid, h = 0
         const double acc = tot[5][tid] / B;
-        const double lprev = a.L[ee];
-        const int cur = a.step[ee] + 1;
+        const int cur = step_prev + 1;
         const double lnew = (loss - lprev) / (lprev + 0.1);
         const bool done = cur >= a.max_steps;
         const bool wipe = done && a.auto_reset;
@@ -177,24 +224,33 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
         wipe_sh[tid] = wipe ? 1 : 0;
     }
     __syncthreads();
+    CE_STAMP(4);
     // per (env, parameter): W', G', obs, or the auto-reset's W0 / zeros
-    for (int i = tid; i < kLrEnvs * P; i += kLrBlock) {
-        const int j = i / P, p = i - j * P;             // env e0 + j, parameter p = 2f + col
+    if (tid < np_) {
+        const int j = tid / P, p = tid - j * P;         // env e0 + j, parameter p = 2f + col
         const int ee = e0 + j;
-        if (ee >= a.E) continue;
-        const bool wipe = wipe_sh[j] != 0;
-        const size_t gi = static_cast<size_t>(ee) * P + p;
-        const int f = p >> 1;
-        // S[f][env j] sits on lane j + 16 (f & 3), register f >> 2
-        const double sf = tot[f >> 2][j + 16 * (f & 3)];
-        const double g = ((p & 1) ? sf : -sf) / B;
-        const double gnew = g / (fabs(a.G[gi]) + 1.0);
-        float *obs = a.obs + static_cast<size_t>(ee) * OBS;
-        obs[p] = 0.0f;                                   // wght_hist is identically 0
-        obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(gnew);
-        a.W[gi] = wipe ? a.W0[gi] : wsh[j][p];
-        a.G[gi] = wipe ? 0.0 : gnew;
+        if (ee < a.E) {
+            const bool wipe = wipe_sh[j] != 0;
+            const size_t gi = static_cast<size_t>(ee) * P + p;
+            const int f = p >> 1;
+            // S[f][env j] sits on lane j + 16 (f & 3), register f >> 2
+            const double sf = tot[f >> 2][j + 16 * (f & 3)];
+            const double g = ((p & 1) ? sf : -sf) / B;
+            const double gnew = g / (fabs(g_prev) + 1.0);
+            float *obs = a.obs + static_cast<size_t>(ee) * OBS;
+            obs[p] = 0.0f;                               // wght_hist is identically 0
+            obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(gnew);
+            a.W[gi] = wipe ? w_init : wsh[j][p];
+            a.G[gi] = wipe ? 0.0 : gnew;
+        }
     }
+#ifdef CE_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    CE_STAMP(5);
+    stamps[7] = __builtin_amdgcn_s_memrealtime();
+    const int row = blockIdx.x * kLrWaves + wave;
+    if (row < a.E && lane < kStamps) a.diag[static_cast<size_t>(row) * kStamps + lane] = stamps[lane];
+#endif
 }
 
 }  // namespace ce

@@ -50,8 +50,14 @@ def main():
     st = np.zeros((E, 8), np.uint64)
     _native.check(lib.ce_diag_stamps(eng._h, st.ctypes.data), 'diag')
     st = st.astype(np.int64)
-    names = ['stage+barrier', 'state loads+bcast', 'row loop', 'reduce+info', 'epilogue']
     res = {'envs': E, 'precision': args.precision}
+    names = ['stage+barrier', 'state loads+bcast', 'row loop', 'reduce+info', 'epilogue']
+    if 'lr_mfma' in eng.step_kernel:
+        # optimize_lr_mfma_kernel: one row per wave (16 envs x 8 waves per workgroup)
+        st = st[:(E + 15) // 16 * 8]
+        names = ['W + first tile loads', 'row tiles', 'partials meet', 'scalar epilogue',
+                 'param epilogue + drain']
+    res['kernel'] = eng.step_kernel
     for k, name in enumerate(names):
         d = st[:, k + 1] - st[:, k]
         res[name] = {'median': float(np.median(d)), 'p90': float(np.percentile(d, 90))}

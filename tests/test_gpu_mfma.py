@@ -24,17 +24,19 @@ def _need_gpu():
         pytest.fail('GPU tests need a ROCm device (run under gpurun)')
 
 
-def _engine(dataset, num_envs, batch_size=None, generic=False, **kw):
+def _engine(dataset, num_envs, batch_size=None, generic=False, lr=False, **kw):
     from custom_envs_amd.engine import OptimizeEngine
-    old = os.environ.get('CE_GENERIC')
-    os.environ['CE_GENERIC'] = '1' if generic else '0'
+    flags = {'CE_GENERIC': '1' if generic else '0', 'CE_LR_MFMA': '1' if lr else '0'}
+    old = {k: os.environ.get(k) for k in flags}
+    os.environ.update(flags)
     try:
         return OptimizeEngine(*dataset, num_envs=num_envs, batch_size=batch_size, **kw)
     finally:
-        if old is None:
-            os.environ.pop('CE_GENERIC')
-        else:
-            os.environ['CE_GENERIC'] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
 
 
 def _classes(n_rows, n_features, n_classes, seed):
@@ -180,7 +182,7 @@ def test_unsupported_shapes_fail_loudly():
 
 # ---------------------------------------------------------------------------
 # The two-class full-batch kernel with envs on the MFMA N dimension
-# (optimize_lr_mfma.h): the default for K = 2, F <= 16, B = N in float64.
+# (optimize_lr_mfma.h; CE_LR_MFMA=1) for K = 2, F <= 16, B = N in float64.
 
 def _two_class(n_rows, n_features, seed):
     rs = np.random.RandomState(seed)
@@ -195,7 +197,7 @@ def test_lr_mfma_kernel_matches_oracle(n_rows, n_features, num_envs):
     """Ragged row tiles (N % 16 != 0), partial 16-env groups, every k-step
     count, many tiles per wave (the cross-entropy product folds)."""
     ds = _two_class(n_rows, n_features, n_rows + n_features)
-    eng = _engine(ds, num_envs, None)
+    eng = _engine(ds, num_envs, None, lr=True)
     assert eng.step_kernel == 'optimize_lr_mfma_kernel<%d>' % ((n_features + 3) // 4)
     envs = sorted({0, num_envs // 2, num_envs - 1})
     _check(ds, None, eng, envs, 43)
@@ -203,17 +205,14 @@ def test_lr_mfma_kernel_matches_oracle(n_rows, n_features, num_envs):
 
 
 def test_lr_mfma_agrees_with_register_kernel(lr_dataset):
-    """Same envs through the MFMA kernel and the two-envs-per-wave register
-    kernel (CE_LR_MFMA=0): float64 results agree to float32 rounding."""
+    """Same envs through the MFMA kernel (CE_LR_MFMA=1) and the default
+    two-envs-per-wave register kernel: float64 results agree to float32
+    rounding."""
     E, T = 64, 45
     acts = np.random.RandomState(3).normal(0, 0.02, (T, E, 20)).astype(np.float32)
     outs = []
     for flag in ('1', '0'):
-        os.environ['CE_LR_MFMA'] = flag
-        try:
-            eng = _engine(lr_dataset, E, None)
-        finally:
-            os.environ.pop('CE_LR_MFMA')
+        eng = _engine(lr_dataset, E, None, lr=flag == '1')
         assert ('lr_mfma' in eng.step_kernel) == (flag == '1')
         eng.seed(list(range(E)))
         eng.reset()
