@@ -91,6 +91,9 @@ struct ce_engine {
     ce_config cfg{};
     int P = 0, obs_dim = 0;
     bool mlp = false;  // CE_PROBLEM_MLP
+    bool mlp_split = false;  // two launches per step (CE_MLP_SPLIT=1 or CE_MLP_PHASES)
+    int n_cus = 1;           // compute units of the device (persistent MLP grid)
+    bool mlp_persist = false;  // CE_MLP_PERSIST=1: the 8-wave persistent step kernel
     int mlp_phases = 3;  // bit 0: train kernel, bit 1: info kernel (CE_MLP_PHASES, profiling)
     size_t tsize = 8;  // element size of W / W0
     size_t gsize = 8;  // element size of G (grad_hist)
@@ -181,6 +184,7 @@ ce::MlpArgs make_mlp_args(const ce_engine *e, const float *act, const ce_outputs
     a.auto_reset = e->cfg.auto_reset;
     a.X = static_cast<const float *>(e->X);
     a.Xs = e->Xs;
+    a.diag = e->diag;
     a.label = e->label;
     a.W = static_cast<float *>(e->W);
     a.W0 = static_cast<const float *>(e->W0);
@@ -205,11 +209,30 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
     if (e->mlp) {
         const ce::MlpArgs a = make_mlp_args(e, act, o);
         const dim3 grid(e->cfg.num_envs), block(ce::kMlpBlock);
+        const bool even = (e->P & 1) == 0;   // pair accesses aligned in every env
         if (reset) {
             hipLaunchKernelGGL(ce::mlp_reset_kernel, grid, block, 0, stream, a);
+        } else if (e->mlp_persist) {
+            // persistent: one 8-wave workgroup per CU (mlp_kernels.h)
+            const dim3 pgrid(std::min(e->cfg.num_envs, e->n_cus)), pblock(ce::kMlpStepBlock);
+            if (even)
+                hipLaunchKernelGGL(ce::mlp_persist_kernel<true>, pgrid, pblock, ce::kMlpStepRingLds,
+                                   stream, a);
+            else
+                hipLaunchKernelGGL(ce::mlp_persist_kernel<false>, pgrid, pblock, ce::kMlpStepRingLds,
+                                   stream, a);
+        } else if (!e->mlp_split) {
+            if (even) hipLaunchKernelGGL(ce::mlp_step_kernel<true>, grid, block, 0, stream, a);
+            else hipLaunchKernelGGL(ce::mlp_step_kernel<false>, grid, block, 0, stream, a);
         } else {
-            if (e->mlp_phases & 1) hipLaunchKernelGGL(ce::mlp_train_kernel, grid, block, 0, stream, a);
-            if (e->mlp_phases & 2) hipLaunchKernelGGL(ce::mlp_info_kernel, grid, block, 0, stream, a);
+            if (e->mlp_phases & 1) {
+                if (even) hipLaunchKernelGGL(ce::mlp_train_kernel<true>, grid, block, 0, stream, a);
+                else hipLaunchKernelGGL(ce::mlp_train_kernel<false>, grid, block, 0, stream, a);
+            }
+            if (e->mlp_phases & 2) {
+                if (even) hipLaunchKernelGGL(ce::mlp_info_kernel<true>, grid, block, 0, stream, a);
+                else hipLaunchKernelGGL(ce::mlp_info_kernel<false>, grid, block, 0, stream, a);
+            }
         }
         return;
     }
@@ -401,7 +424,10 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     if (const char *ph = std::getenv("CE_MLP_PHASES")) {
         if (std::strcmp(ph, "train") == 0) e->mlp_phases = 1;
         if (std::strcmp(ph, "info") == 0) e->mlp_phases = 2;
+        e->mlp_split = true;
     }
+    if (const char *sp = std::getenv("CE_MLP_SPLIT")) e->mlp_split = e->mlp_split || sp[0] == '1';
+    if (const char *pp = std::getenv("CE_MLP_PERSIST")) e->mlp_persist = !e->mlp_split && pp[0] == '1';
     if (mlp) {
         const int F = cfg->n_features, H = cfg->n_hidden, K = cfg->n_classes;
         e->P = F * H + H + H * K + K;
@@ -431,6 +457,12 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
 
     const size_t E = cfg->num_envs, N = cfg->n_rows, F = cfg->n_features, P = e->P;
     if (mlp) {
+        CE_TRY(hipDeviceGetAttribute(&e->n_cus, hipDeviceAttributeMultiprocessorCount, cfg->device));
+        const int lds = static_cast<int>(ce::kMlpStepRingLds);
+        CE_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(ce::mlp_persist_kernel<true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        CE_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(ce::mlp_persist_kernel<false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         CE_TRY(hipMalloc(&e->X, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->Xs, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
@@ -711,7 +743,9 @@ int ce_step_many_prepare(ce_engine *e, int32_t k, const float *actions, int64_t 
 
 const char *ce_step_kernel(const ce_engine *e) {
     if (!e) return "";
-    if (e->mlp) return "mlp_train_kernel+mlp_info_kernel";
+    if (e->mlp)
+        return e->mlp_split ? "mlp_train_kernel+mlp_info_kernel"
+                            : e->mlp_persist ? "mlp_persist_kernel" : "mlp_step_kernel";
     return e->kernel_name.c_str();
 }
 

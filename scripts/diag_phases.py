@@ -26,6 +26,7 @@ def main():
     p.add_argument('--envs', type=int, default=4096)
     p.add_argument('--precision', default='f64')
     p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--workload', default='optimize', choices=['optimize', 'mlp'])
     args = p.parse_args()
     assert os.environ.get('CE_LIB', '').startswith('diag'), 'run with CE_LIB=diag*'
     import torch
@@ -34,18 +35,23 @@ def main():
     from custom_envs_amd.engine import OptimizeEngine
     lib = _native.load()
     lib.ce_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    seq = load_data('gaussians_256x10', batch_size=None)
     E = args.envs
-    eng = OptimizeEngine(seq.features, seq.targets, num_envs=E, precision=args.precision)
+    if args.workload == 'mlp':
+        from bench import mlp_dataset
+        features, targets = mlp_dataset()
+        eng = OptimizeEngine(features, targets, num_envs=E, batch_size=32, model='mlp')
+    else:
+        seq = load_data('gaussians_256x10', batch_size=None)
+        eng = OptimizeEngine(seq.features, seq.targets, num_envs=E, precision=args.precision)
     eng.seed(list(range(E)))
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
     out = eng.alloc_device_outputs()
-    acts = torch.randn((args.steps, E, eng.act_dim), device='cuda') * 0.01
+    acts = torch.randn((2, E, eng.act_dim), device='cuda') * 0.01
     eng.reset_device(out)
     for s in range(args.steps):
-        eng.step_device(acts[s], out)
+        eng.step_device(acts[s % 2], out)
     torch.cuda.synchronize()
     st = np.zeros((E, 8), np.uint64)
     _native.check(lib.ce_diag_stamps(eng._h, st.ctypes.data), 'diag')
@@ -57,6 +63,18 @@ def main():
         st = st[:(E + 15) // 16 * 8]
         names = ['W + first tile loads', 'row tiles', 'partials meet', 'scalar epilogue',
                  'param epilogue + drain']
+    if 'mlp' in eng.step_kernel:
+        # mlp_step_kernel: train half stamps 0-3, info half 4-6 of the same env
+        names = ['forward', 'softmax + small grads', 'dW1 + G/obs', 'train end -> info start',
+                 'info passes', 'info epilogue + drain']
+        res['kernel'] = eng.step_kernel
+        for k, name in enumerate(names):
+            d = st[:, k + 1] - st[:, k]
+            res[name] = {'median': float(np.median(d)), 'p90': float(np.percentile(d, 90))}
+        res['train_median'] = float(np.median(st[:, 3] - st[:, 0]))
+        res['info_median'] = float(np.median(st[:, 6] - st[:, 4]))
+        print(json.dumps(res))
+        return
     res['kernel'] = eng.step_kernel
     for k, name in enumerate(names):
         d = st[:, k + 1] - st[:, k]

@@ -188,3 +188,75 @@ def test_make_optimize_mlp_env():
         assert reward < 0 and info['episode']['l'] == 1
     finally:
         env.close()
+
+
+@pytest.mark.parametrize('n_classes', [11, 10])
+def test_odd_parameter_blocks_against_live_oracle(n_classes):
+    """K = 11 makes P odd, so every odd env's parameter block starts at an odd
+    float and takes the split pair accesses (mlp_kernels.h ld_f2/st_d2);
+    F = 40 leaves a partial dW1 feature tile and a 5-chunk forward."""
+    from oracle.gen_golden import mlp_dataset
+    features, targets = mlp_dataset(n_rows=192, n_features=40, n_classes=n_classes)
+    seeds = [3, 4, 5]
+    eng = _engine(features, targets, len(seeds))
+    refs = []
+    for s in seeds:
+        env = OracleEnv(features, targets, batch_size=32, model='mlp')
+        env.seed(s)
+        env.reset()
+        refs.append(env)
+    try:
+        eng.seed(seeds)
+        eng.reset()
+        P = eng.act_dim
+        assert P == 40 * 64 + 64 + 64 * n_classes + n_classes
+        rs = np.random.RandomState(31)
+        for t in range(43):
+            acts = rs.normal(0, 1e-3, (len(seeds), P)).astype(np.float32)
+            out = eng.step(acts)
+            for i, env in enumerate(refs):
+                obs, reward, done, info = env.step(acts[i])
+                if done:
+                    obs = env.reset()
+                assert bool(out['done'][i]) == done
+                _row_close(out['obs'][i], obs)
+                assert _rel(out['reward'][i], reward) <= RTOL
+                assert _rel(out['objective'][i], info['objective']) <= RTOL
+                assert out['accuracy'][i] == np.float32(info['accuracy'])
+            if not out['done'].any():
+                w = eng.get_state()['weights'].astype(np.float32)
+                for i, env in enumerate(refs):
+                    assert np.array_equal(w[i], env.model.weights.astype(np.float32)), (t, i)
+    finally:
+        eng.close()
+
+
+def test_fused_step_matches_split_kernels(monkeypatch):
+    """mlp_step_kernel (one launch) and the split train + info pair run the
+    same arithmetic: bit-identical outputs, except the objective, whose
+    per-wave partial sums cover different tile sets (4 vs 8 tiles per pass)."""
+    from oracle.gen_golden import mlp_dataset
+    features, targets = mlp_dataset(n_rows=256, n_features=64)
+    E = 37
+    fused = _engine(features, targets, E)
+    monkeypatch.setenv('CE_MLP_SPLIT', '1')
+    split = _engine(features, targets, E)
+    try:
+        assert fused.step_kernel == 'mlp_step_kernel'
+        assert split.step_kernel == 'mlp_train_kernel+mlp_info_kernel'
+        for eng in (fused, split):
+            eng.seed(list(range(E)))
+            eng.reset()
+        rs = np.random.RandomState(5)
+        for t in range(41):
+            acts = rs.normal(0, 1e-3, (E, fused.act_dim)).astype(np.float32)
+            a = {k: v.copy() for k, v in fused.step(acts).items()}
+            b = split.step(acts)
+            for k in a:
+                if k == 'objective':
+                    np.testing.assert_allclose(a[k], b[k], rtol=1e-6, err_msg=str(t))
+                else:
+                    assert np.array_equal(a[k], b[k]), (t, k)
+    finally:
+        fused.close()
+        split.close()
