@@ -123,6 +123,7 @@ struct ce_engine {
     std::string kernel_name;  // what ce_step_kernel reports
     size_t stage_bytes = 0;
     ce::GraphCache graphs;   // ce_step_many
+    int many_direct = 0;     // ce_step_many: k <= many_direct -> plain launches, no graph
     unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
 };
 
@@ -420,6 +421,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     e->cfg = *cfg;
     e->kern = kern;
     e->mlp = mlp;
+    if (const char *md = std::getenv("CE_MANY_DIRECT")) e->many_direct = std::atoi(md);
     // experiment switch: launch one phase only, to time each kernel alone
     if (const char *ph = std::getenv("CE_MLP_PHASES")) {
         if (std::strcmp(ph, "train") == 0) e->mlp_phases = 1;
@@ -728,6 +730,15 @@ int many_graph(ce_engine *e, int32_t k, const float *actions, int64_t stride,
 
 int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
                  const ce_outputs *out) {
+    if (e && k <= e->many_direct) {
+        if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
+        if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "ce_step_many: bad arguments");
+        if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+        const ce_outputs o = out ? *out : region_view(e, e->d_out);
+        for (int s = 0; s < k; ++s) launch(e, false, actions + s * stride, o, e->stream);
+        CE_HIP(hipGetLastError());
+        return CE_OK;
+    }
     hipGraphExec_t exec;
     const int rc = many_graph(e, k, actions, stride, out, &exec);
     if (rc != CE_OK) return rc;

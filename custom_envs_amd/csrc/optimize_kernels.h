@@ -406,12 +406,13 @@ __device__ __forceinline__ T exp_neg(T a, const MathConsts<T> &) {
 // and forced to three-operand v_fma_f64: left to itself the compiler keeps
 // the coefficients in VGPRs and emits a v_mov_b64 copy before every
 // two-operand v_fmac_f64 (10 extra instructions per exp).
+// exp_neg_multi_clamped takes arguments already in [0, 750].
 template <int Q>
-__device__ __forceinline__ void exp_neg_multi(double (&a)[Q]) {
+__device__ __forceinline__ void exp_neg_multi_clamped(double (&a)[Q]) {
     double m[Q], r[Q], q[Q];
 #pragma unroll
     for (int i = 0; i < Q; ++i) {
-        const double x = fmin(a[i], 750.0);
+        const double x = a[i];
         m[i] = rint(x * -kLog2e);
         r[i] = fma(m[i], -kLn2Lo, fma(m[i], -kLn2Hi, -x));
         q[i] = kExpCoef[kExpTerms - 1];
@@ -425,6 +426,19 @@ __device__ __forceinline__ void exp_neg_multi(double (&a)[Q]) {
     }
 #pragma unroll
     for (int i = 0; i < Q; ++i) a[i] = ldexp(q[i], static_cast<int>(m[i]));
+}
+template <int Q>
+__device__ __forceinline__ void exp_neg_multi(double (&a)[Q]) {
+#pragma unroll
+    for (int i = 0; i < Q; ++i) a[i] = fmin(a[i], 750.0);
+    exp_neg_multi_clamped<Q>(a);
+}
+// min(|u|, 750) in one v_min_f64 (fmin(fabs(u), 750) of an MFMA result gets a
+// canonicalising v_max_f64 first)
+__device__ __forceinline__ double abs_clamp750(double u) {
+    double r;
+    asm("v_min_f64 %0, |%1|, %2" : "=v"(r) : "v"(u), "v"(750.0));
+    return r;
 }
 
 // float32 engine: hardware v_exp_f32 (about 1 ulp of float).
@@ -524,6 +538,56 @@ struct TwoClassModel {
 #pragma unroll
             for (int f = 0; f < F; ++f) acc[f] = fma(x[f], q, acc[f]);
         }
+    }
+
+    // `row` for UU rows at once, float64, every stage of the UU rows issued
+    // side by side (margins, exp chains, reciprocals, then the gradient
+    // FMAs): one row's ~30-deep dependent chain is otherwise issued back to
+    // back, each f64 step waiting out the ~10-cycle dependent latency.
+    template <bool MASKED, int UU, int NA>
+    static __device__ __forceinline__ void rows_multi(const T (&x)[UU][F], const T (&wd)[NB],
+                                                      const bool (&valid)[UU], T (&acc)[NA],
+                                                      T &prod, int &hits, Watch &wt) {
+        static_assert(std::is_same<T, double>::value, "float64 rows only");
+        double u[UU], t[UU];
+#pragma unroll
+        for (int i = 0; i < UU; ++i) u[i] = x[i][0] * wd[0];
+#pragma unroll
+        for (int f = 1; f < F; ++f)
+#pragma unroll
+            for (int i = 0; i < UU; ++i) u[i] = fma(x[i][f], wd[f], u[i]);
+#pragma unroll
+        for (int i = 0; i < UU; ++i) t[i] = fabs(u[i]);
+        exp_neg_multi<UU>(t);
+        double d[UU], r[UU], e[UU];
+#pragma unroll
+        for (int i = 0; i < UU; ++i) {
+            d[i] = 1.0 + t[i];
+            r[i] = __builtin_amdgcn_rcp(d[i]);
+        }
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {                    // two Newton steps: <= 1 ulp
+#pragma unroll
+            for (int i = 0; i < UU; ++i) e[i] = fma(-d[i], r[i], 1.0);
+#pragma unroll
+            for (int i = 0; i < UU; ++i) r[i] = fma(r[i], e[i], r[i]);
+        }
+        double q[UU];
+#pragma unroll
+        for (int i = 0; i < UU; ++i) {
+            const double inv = r[i];                     // p of the larger-logit class
+            const double lo = t[i] * inv;                // p of the other class
+            const bool neg = u[i] < 0.0;
+            const bool ok = !MASKED || valid[i];
+            q[i] = ok ? (neg ? inv : lo) : 0.0;
+            prod *= ok ? (neg ? lo : inv) + 1e-16 : 1.0;
+            wt.tmax = fmax(wt.tmax, ok ? t[i] : 0.0);
+            hits += (ok && u[i] > 0.0) ? 1 : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < UU; ++i)
+#pragma unroll
+            for (int f = 0; f < F; ++f) acc[f] = fma(x[i][f], q[i], acc[f]);
     }
 
     // The first-maximum argmax of a tied row (t == 1): hit iff y == 0.

@@ -51,7 +51,10 @@ __host__ __device__ constexpr int lr_tile_doubles(int nkf) { return (nkf + 4 + 2
 //   [nkf + 5]  int32 pair: q = 2, 3
 // (layout [tile][slot][lane]; built by the engine at ce_create)
 
-template <int NKF>
+// PAD: N is not a multiple of 16, so the last tile has padding rows
+// (label -1) that every per-item statistic must skip; with PAD false the
+// row loop reads no labels at all (the sign-folded rows carry y).
+template <int NKF, bool PAD>
 __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<double> a) {
     constexpr int P_MAX = 2 * kLrMaxF;
     constexpr int TD = lr_tile_doubles(NKF);
@@ -75,26 +78,20 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     const double *img = reinterpret_cast<const double *>(a.data);
     const int ntiles = (N + 15) / 16;
 
-    // ---- W' = W - a (optimize.py:74-75); forward B operand: the margin
-    // w'_f0 - w'_f1 of feature 4k + h for env c
-    double wd[NKF];
+    // ---- every state load of the step issued before any is used (one
+    // memory round trip): W and the action of features 4k + h of env c
+    // (forward B operand), then the epilogue's per (env, parameter) G and
+    // W0 and per env L and the step counter
+    double2 wv[NKF];
+    float av0[NKF], av1[NKF];
 #pragma unroll
     for (int k = 0; k < NKF; ++k) {
         const int f = 4 * k + h;
-        const bool own = f < F;
-        const size_t i0 = pbase + (own ? 2 * f : 0);
-        const double w0 = a.W[i0] - static_cast<double>(a.act[i0]);
-        const double w1 = a.W[i0 + 1] - static_cast<double>(a.act[i0 + 1]);
-        wd[k] = own ? w0 - w1 : 0.0;
-        if (wave == 0 && own) {                         // kept for the epilogue
-            wsh[c][2 * f] = w0;
-            wsh[c][2 * f + 1] = w1;
-        }
+        const size_t i0 = pbase + (f < F ? 2 * f : 0);
+        wv[k] = *reinterpret_cast<const double2 *>(a.W + i0);   // 16-B aligned: P even
+        av0[k] = a.act[i0];
+        av1[k] = a.act[i0 + 1];
     }
-
-    // ---- the epilogue's state loads, issued now so their latency hides
-    // under the row work: per (env, parameter) thread G and W0, per env L
-    // and the step counter
     const int tid = threadIdx.x;
     const int B = a.B;
     const int np_ = kLrEnvs * P;
@@ -110,27 +107,46 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     const double lprev = a.L[es < a.E ? es : 0];
     const int step_prev = a.step[es < a.E ? es : 0];
 
-    lr_d4 s = {0.0, 0.0, 0.0, 0.0};
-    double prod = 1.0, nlog = 0.0;
-    int hits = 0;
-    int since = 0;
     // the wave's row tiles, each one's operands loaded a tile ahead
     double xf[NKF], xg[4];
-    int2 y01, y23;
+    int2 y01 = {0, 0}, y23 = {0, 0};
     auto load_tile = [&](int t) {
         const double *ti = img + static_cast<size_t>(t) * TD;
 #pragma unroll
         for (int k = 0; k < NKF; ++k) xf[k] = ti[k * kWave + lane];
 #pragma unroll
         for (int q = 0; q < 4; ++q) xg[q] = ti[(NKF + q) * kWave + lane];
-        y01 = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
-        y23 = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
+        if constexpr (PAD) {
+            y01 = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
+            y23 = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
+        }
     };
     if (wave < ntiles) load_tile(wave);
+
+    // ---- W' = W - a (optimize.py:74-75); forward B operand: the margin
+    // w'_f0 - w'_f1 of feature 4k + h for env c
+    double wd[NKF];
+#pragma unroll
+    for (int k = 0; k < NKF; ++k) {
+        const int f = 4 * k + h;
+        const bool own = f < F;
+        const double w0 = wv[k].x - static_cast<double>(av0[k]);
+        const double w1 = wv[k].y - static_cast<double>(av1[k]);
+        wd[k] = own ? w0 - w1 : 0.0;
+        if (wave == 0 && own) {                         // kept for the epilogue
+            wsh[c][2 * f] = w0;
+            wsh[c][2 * f + 1] = w1;
+        }
+    }
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     CE_STAMP(1);
+
+    lr_d4 s = {0.0, 0.0, 0.0, 0.0};
+    double prod = 1.0, nlog = 0.0, tmax = 0.0;
+    int hits = 0;
+    int since = 0;
 #if defined(CE_LR_EXP) && (CE_LR_EXP == 1 || CE_LR_EXP == 3)
     for (int t = ntiles; t < ntiles; t += kLrWaves) {     // experiment: no row work
 #else
@@ -152,12 +168,13 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
 #pragma unroll
         for (int k = 0; k < NKF; ++k) u = __builtin_amdgcn_mfma_f64_16x16x4f64(cf[k], wd[k], u, 0, 0, 0);
         // two-class softmax of TwoClassModel per (row, env): t = e^-|u|,
-        // p of the larger logit 1/(1+t); q = 1 - p_y (the gradient weight);
-        // a tie (t == 1, p0 == p1) is np.argmax's class 0: hit iff y == 0
+        // p of the larger logit 1/(1+t); q = 1 - p_y (the gradient weight).
+        // Argmax hit = u > 0 except on a tie (t == 1), which max(t) flags
+        // for the exact pass after the loop.
         double tx[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tx[q] = fabs(u[q]);
-        exp_neg_multi<4>(tx);                           // t = e^-|u|, 4 chains interleaved
+        for (int q = 0; q < 4; ++q) tx[q] = abs_clamp750(u[q]);
+        exp_neg_multi_clamped<4>(tx);                   // t = e^-|u|, 4 chains interleaved
         double qv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -166,14 +183,35 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
             const double inv = rcp_unit(1.0 + tq);
             const double lo = tq * inv;
             const bool neg = uq < 0.0;
-            const bool valid = ys[q] >= 0;
+            const bool valid = !PAD || ys[q] >= 0;
             qv[q] = valid ? (neg ? inv : lo) : 0.0;
             prod *= valid ? (neg ? lo : inv) + 1e-16 : 1.0;
-            const bool hit = tq == 1.0 ? ys[q] == 0 : uq > 0.0;
-            hits += (valid && hit) ? 1 : 0;
+            tmax = fmax(tmax, valid ? tq : 0.0);
+            hits += (valid && uq > 0.0) ? 1 : 0;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) s = __builtin_amdgcn_mfma_f64_16x16x4f64(cg[q], qv[q], s, 0, 0, 0);
+    }
+    // a tie (p0 == p1) is np.argmax's class 0: hit iff y == 0.  Only a wave
+    // that saw t == 1 re-walks its tiles (practically never: |z| < 2^-53).
+    if (__any(tmax == 1.0)) {
+        for (int t = wave; t < ntiles; t += kLrWaves) {
+            const double *ti = img + static_cast<size_t>(t) * TD;
+            lr_d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < NKF; ++k)
+                u = __builtin_amdgcn_mfma_f64_16x16x4f64(ti[k * kWave + lane], wd[k], u, 0, 0, 0);
+            const int2 ya = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
+            const int2 yb = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
+            const int ys[4] = {ya.x, ya.y, yb.x, yb.y};
+            double tx[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tx[q] = abs_clamp750(u[q]);
+            exp_neg_multi_clamped<4>(tx);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (ys[q] >= 0 && tx[q] == 1.0) hits += (ys[q] == 0 ? 1 : 0) - (u[q] > 0.0 ? 1 : 0);
+        }
     }
     // partials of this wave: s (features h + 4r of env c), -log of the
     // cross-entropy factors, hits

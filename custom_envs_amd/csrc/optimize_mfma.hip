@@ -39,7 +39,12 @@ static_assert(16 == kGenMaxF / 4, "one instance per k-step count");
 template <int NKF>
 void launch_lr(const StepArgs<double> &a, hipStream_t stream) {
     const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
-    hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF>), dim3(grid), dim3(kLrBlock), 0, stream, a);
+    if (a.N % 16 == 0)
+        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, false>), dim3(grid), dim3(kLrBlock), 0,
+                           stream, a);
+    else
+        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, true>), dim3(grid), dim3(kLrBlock), 0,
+                           stream, a);
 }
 constexpr GenFn kLrSteps[4] = {launch_lr<1>, launch_lr<2>, launch_lr<3>, launch_lr<4>};
 

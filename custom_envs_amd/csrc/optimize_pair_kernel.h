@@ -73,6 +73,10 @@ __device__ __forceinline__ void pair_rows(const T *xs, const int32_t *ys, const 
         r[u] = valid[u] ? (ORDERED ? order[iu] : iu) : 0;
         load_row<T, F>(xs, r[u], x[u]);
     }
+    if constexpr (!FIX && Model::kProd) {
+        Model::template rows_multi<MASKED, UU>(x, w, valid, acc, prod, hits, wt);
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         if constexpr (FIX)

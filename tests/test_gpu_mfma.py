@@ -223,3 +223,19 @@ def test_lr_mfma_agrees_with_register_kernel(lr_dataset):
         assert np.array_equal(a['done'], b['done'])
         assert np.array_equal(a['episode_len'], b['episode_len'])
         assert np.array_equal(a['accuracy'], b['accuracy'])
+
+
+@pytest.mark.parametrize('n_rows', [256, 203])
+@pytest.mark.parametrize('lr', [True, False])
+def test_two_class_ties_take_class_zero(n_rows, lr):
+    """Zero rows give z = 0 exactly, a probability tie whatever the weights:
+    np.argmax then picks class 0, so such a row is a hit iff y == 0.  The
+    two-class kernels count hits as z > 0 and re-walk a wave's rows only when
+    max(t) == 1 flags a tie (the LR MFMA kernel with and without padding
+    rows, and the register pair kernel)."""
+    x, y = _two_class(n_rows, 10, 5)
+    x[::7] = 0.0                       # ties, of both labels
+    eng = _engine((x, y), 19, None, lr=lr)
+    assert ('lr_mfma' in eng.step_kernel) == lr
+    _check((x, y), None, eng, [0, 9, 18], 12)
+    eng.close()
