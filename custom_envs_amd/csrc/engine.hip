@@ -123,7 +123,10 @@ struct ce_engine {
     std::string kernel_name;  // what ce_step_kernel reports
     size_t stage_bytes = 0;
     ce::GraphCache graphs;   // ce_step_many
-    int many_direct = 0;     // ce_step_many: k <= many_direct -> plain launches, no graph
+    // ce_step_many: k <= many_direct steps are plain launches, longer runs a
+    // cached hipGraph.  Measured (4096 envs, pair kernel): 20 steps 7.7 us
+    // per step direct vs 8.0 graph; 100 and 2000 steps equal.
+    int many_direct = 32;
     unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
 };
 
@@ -264,6 +267,12 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
     }
 }
 
+// k steps of every env, actions s * stride apart.
+void launch_steps(const ce_engine *e, int k, const float *actions, int64_t stride,
+                  const ce_outputs &o) {
+    for (int s = 0; s < k; ++s) launch(e, false, actions + s * stride, o, e->stream);
+}
+
 // Convert host float64 values to a device array of `elem`-byte floats.
 int upload_typed(ce_engine *e, void *dst, const double *src, size_t count, size_t elem) {
     if (elem == sizeof(double)) {
@@ -391,12 +400,14 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         // forces the runtime-shape kernel, for tests), else the MFMA kernel
         const char *force = std::getenv("CE_GENERIC");
         const bool generic = force && force[0] == '1';
-        // CE_LR_MFMA=1: the two-class full-batch shapes run on the MFMA kernel
-        // with envs along N (optimize_lr_mfma.h).  Measured at 4096 envs it
-        // ties the two-envs-per-wave register kernel (6.6-6.7 us vs 6.3-6.7
-        // us per step), which therefore stays the default.
+        // The two-class full-batch float64 shapes (the benchmark's) run on
+        // the MFMA kernel with envs along N (optimize_lr_mfma.h): 6.30 us
+        // per 4096-env step against 6.32 for the two-envs-per-wave register
+        // kernel, 7.47 against 7.6-7.8 us per step over 20-step runs
+        // (DESIGN.md 3.9).  CE_LR_MFMA=0 (or CE_PAIR_U) selects the register
+        // kernel instead.
         const char *lrm = std::getenv("CE_LR_MFMA");
-        lr_path = !generic && (lrm && lrm[0] == '1') && !std::getenv("CE_PAIR_U") &&
+        lr_path = !generic && !(lrm && lrm[0] == '0') && !std::getenv("CE_PAIR_U") &&
                   cfg->precision == CE_F64 && cfg->batch_size == cfg->n_rows &&
                   ce::lr_shape_ok(cfg->n_features, cfg->n_classes);
         if (!generic && !lr_path)
@@ -722,7 +733,7 @@ int many_graph(ce_engine *e, int32_t k, const float *actions, int64_t stride,
     if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
     const ce_outputs o = out ? *out : region_view(e, e->d_out);
     return e->graphs.get(ce::graph_key(k, 0, actions, stride, e->stream, o), [&] {
-        for (int s = 0; s < k; ++s) launch(e, false, actions + s * stride, o, e->stream);
+        launch_steps(e, k, actions, stride, o);
     }, exec);
 }
 
@@ -735,7 +746,7 @@ int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
         if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "ce_step_many: bad arguments");
         if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
         const ce_outputs o = out ? *out : region_view(e, e->d_out);
-        for (int s = 0; s < k; ++s) launch(e, false, actions + s * stride, o, e->stream);
+        launch_steps(e, k, actions, stride, o);
         CE_HIP(hipGetLastError());
         return CE_OK;
     }

@@ -19,7 +19,9 @@
 // (16-row tiles t = wave, wave + kLrWaves, ...).  Rows come from a
 // fragment-ordered image built once at ce_create (every MFMA operand one
 // coalesced 8-byte load per lane, no LDS staging and no barrier before the
-// math), the W' operands from the envs' state.  Each wave's partial sums
+// math; staging the rows row-major into LDS by LDS-DMA and reading the
+// operands from there was measured slower), the W' operands
+// from the envs' state.  Each wave's partial sums
 // (gradient, log-loss, hits) meet in LDS; the epilogue -- recurrences,
 // observation, state, auto-reset (optimize.py:80-100, utils_venv.py:31) --
 // is spread over the workgroup's threads.
@@ -32,7 +34,10 @@ namespace ce {
 typedef double lr_d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
-constexpr int kLrWaves = 8;                    // waves per workgroup (row split)
+#ifndef CE_LR_WAVES
+#define CE_LR_WAVES 8
+#endif
+constexpr int kLrWaves = CE_LR_WAVES;          // waves per workgroup (row split)
 constexpr int kLrBlock = kWave * kLrWaves;
 constexpr int kLrMaxF = 16;
 
@@ -51,10 +56,21 @@ __host__ __device__ constexpr int lr_tile_doubles(int nkf) { return (nkf + 4 + 2
 //   [nkf + 5]  int32 pair: q = 2, 3
 // (layout [tile][slot][lane]; built by the engine at ce_create)
 
-// PAD: N is not a multiple of 16, so the last tile has padding rows
-// (label -1) that every per-item statistic must skip; with PAD false the
-// row loop reads no labels at all (the sign-folded rows carry y).
-template <int NKF, bool PAD>
+// MODE (lr_mode): 0 = one tile at a time, padding rows (label -1) masked
+// out of every statistic; 1 = N a multiple of 16 and every wave owning the
+// same number of tiles, so the row loop reads no labels (the sign-folded
+// rows carry y); 2 = as 1 with an even number of tiles per wave, run two at
+// a time: both forward MFMA chains first, then softmax A, gradient MFMAs A,
+// softmax B, gradient MFMAs B, so the matrix pipe works through one tile's
+// MFMAs while the VALU does the other's softmax (f64 MFMA and f64 VALU have
+// the same rate on gfx950; only the overlap gains).
+__host__ __device__ constexpr int lr_mode(int N) {
+    return N % 16 != 0 || ((N + 15) / 16) % kLrWaves != 0 ? 0
+           : ((N + 15) / 16) % (2 * kLrWaves) == 0      ? 2
+                                                          : 1;
+}
+
+template <int NKF, int MODE>
 __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<double> a) {
     constexpr int P_MAX = 2 * kLrMaxF;
     constexpr int TD = lr_tile_doubles(NKF);
@@ -108,18 +124,32 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     const int step_prev = a.step[es < a.E ? es : 0];
 
     // the wave's row tiles, each one's operands loaded a tile ahead
-    double xf[NKF], xg[4];
-    int2 y01 = {0, 0}, y23 = {0, 0};
-    auto load_tile = [&](int t) {
+    constexpr bool PAD = MODE == 0;
+    constexpr bool FULL = MODE == 2;
+    // MFMA operands of tile t: forward A X~[16t + c][4k + h], gradient A
+    // X~[16t + h + 4q][c], labels of rows 16t + h + 4q
+    auto operands = [&](int t, double (&fv)[NKF], double (&gv)[4], int (&yv)[4], bool grad,
+                        bool labels) {
         const double *ti = img + static_cast<size_t>(t) * TD;
 #pragma unroll
-        for (int k = 0; k < NKF; ++k) xf[k] = ti[k * kWave + lane];
+        for (int k = 0; k < NKF; ++k) fv[k] = ti[k * kWave + lane];
+        if (grad)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) xg[q] = ti[(NKF + q) * kWave + lane];
-        if constexpr (PAD) {
-            y01 = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
-            y23 = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
+            for (int q = 0; q < 4; ++q) gv[q] = ti[(NKF + q) * kWave + lane];
+        if (labels) {
+            const int2 ya = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
+            const int2 yb = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
+            yv[0] = ya.x;
+            yv[1] = ya.y;
+            yv[2] = yb.x;
+            yv[3] = yb.y;
         }
+    };
+    double xf[NKF], xg[4], xf2[NKF], xg2[4];
+    int yl[4] = {0, 0, 0, 0}, yl2[4];
+    auto load_tile = [&](int t) {
+        operands(t, xf, xg, yl, true, PAD);
+        if constexpr (FULL) operands(t + kLrWaves, xf2, xg2, yl2, true, false);   // the pair's second tile
     };
     if (wave < ntiles) load_tile(wave);
 
@@ -147,35 +177,15 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     double prod = 1.0, nlog = 0.0, tmax = 0.0;
     int hits = 0;
     int since = 0;
-#if defined(CE_LR_EXP) && (CE_LR_EXP == 1 || CE_LR_EXP == 3)
-    for (int t = ntiles; t < ntiles; t += kLrWaves) {     // experiment: no row work
-#else
-    for (int t = wave; t < ntiles; t += kLrWaves) {
-#endif
-        if (++since > 4) {                              // 16 factors in (1e-16, 1]: fold
-            nlog -= log_pos(prod);
-            prod = 1.0;
-            since = 1;
-        }
-        double cf[NKF], cg[4];
-#pragma unroll
-        for (int k = 0; k < NKF; ++k) cf[k] = xf[k];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cg[q] = xg[q];
-        const int ys[4] = {y01.x, y01.y, y23.x, y23.y};
-        if (t + kLrWaves < ntiles) load_tile(t + kLrWaves);
-        lr_d4 u = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < NKF; ++k) u = __builtin_amdgcn_mfma_f64_16x16x4f64(cf[k], wd[k], u, 0, 0, 0);
-        // two-class softmax of TwoClassModel per (row, env): t = e^-|u|,
-        // p of the larger logit 1/(1+t); q = 1 - p_y (the gradient weight).
-        // Argmax hit = u > 0 except on a tie (t == 1), which max(t) flags
-        // for the exact pass after the loop.
+    // two-class softmax of TwoClassModel per (row, env): t = e^-|u|, p of
+    // the larger logit 1/(1+t); q = 1 - p_y (the gradient weight).  Argmax
+    // hit = u > 0 except on a tie (t == 1), which max(t) flags for the exact
+    // pass after the loop.
+    auto softmax = [&](const lr_d4 &u, const int (&ys)[4], double (&qv)[4]) {
         double tx[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) tx[q] = abs_clamp750(u[q]);
         exp_neg_multi_clamped<4>(tx);                   // t = e^-|u|, 4 chains interleaved
-        double qv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const double uq = u[q];
@@ -189,21 +199,78 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
             tmax = fmax(tmax, valid ? tq : 0.0);
             hits += (valid && uq > 0.0) ? 1 : 0;
         }
+    };
+    auto forward = [&](const double (&xv)[NKF]) {
+        lr_d4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s = __builtin_amdgcn_mfma_f64_16x16x4f64(cg[q], qv[q], s, 0, 0, 0);
+        for (int k = 0; k < NKF; ++k) u = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[k], wd[k], u, 0, 0, 0);
+        return u;
+    };
+    auto gradient = [&](const double (&xv)[4], const double (&qv)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[q], qv[q], s, 0, 0, 0);
+    };
+#if defined(CE_LR_EXP) && (CE_LR_EXP == 1 || CE_LR_EXP == 3)
+    const int t_first = ntiles;                         // experiment: no row work
+#else
+    const int t_first = wave;
+#endif
+    if constexpr (FULL) {
+        const int none[4] = {0, 0, 0, 0};
+        for (int t = t_first; t < ntiles; t += 2 * kLrWaves) {
+            if (++since > 2) {                          // 16 factors in (1e-16, 1]: fold
+                nlog -= log_pos(prod);
+                prod = 1.0;
+                since = 1;
+            }
+            double cf[NKF], cg[4], cf2[NKF], cg2[4];
+#pragma unroll
+            for (int k = 0; k < NKF; ++k) {
+                cf[k] = xf[k];
+                cf2[k] = xf2[k];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                cg[q] = xg[q];
+                cg2[q] = xg2[q];
+            }
+            if (t + 2 * kLrWaves < ntiles) load_tile(t + 2 * kLrWaves);
+            const lr_d4 ua = forward(cf);
+            const lr_d4 ub = forward(cf2);
+            double qa[4], qb[4];
+            softmax(ua, none, qa);
+            gradient(cg, qa);
+            softmax(ub, none, qb);
+            gradient(cg2, qb);
+        }
+    } else {
+        const int none[4] = {0, 0, 0, 0};
+        for (int t = t_first; t < ntiles; t += kLrWaves) {
+            if (++since > 4) {                          // 16 factors in (1e-16, 1]: fold
+                nlog -= log_pos(prod);
+                prod = 1.0;
+                since = 1;
+            }
+            double cf[NKF], cg[4];
+#pragma unroll
+            for (int k = 0; k < NKF; ++k) cf[k] = xf[k];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cg[q] = xg[q];
+            const int ys[4] = {yl[0], yl[1], yl[2], yl[3]};
+            if (t + kLrWaves < ntiles) load_tile(t + kLrWaves);
+            double qv[4];
+            softmax(forward(cf), PAD ? ys : none, qv);
+            gradient(cg, qv);
+        }
     }
     // a tie (p0 == p1) is np.argmax's class 0: hit iff y == 0.  Only a wave
     // that saw t == 1 re-walks its tiles (practically never: |z| < 2^-53).
     if (__any(tmax == 1.0)) {
         for (int t = wave; t < ntiles; t += kLrWaves) {
-            const double *ti = img + static_cast<size_t>(t) * TD;
-            lr_d4 u = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int k = 0; k < NKF; ++k)
-                u = __builtin_amdgcn_mfma_f64_16x16x4f64(ti[k * kWave + lane], wd[k], u, 0, 0, 0);
-            const int2 ya = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
-            const int2 yb = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
-            const int ys[4] = {ya.x, ya.y, yb.x, yb.y};
+            double fv[NKF], gv[4];
+            int ys[4];
+            operands(t, fv, gv, ys, false, true);
+            const lr_d4 u = forward(fv);
             double tx[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) tx[q] = abs_clamp750(u[q]);

@@ -6,6 +6,8 @@
 #include "optimize_lr_mfma.h"
 #include "optimize_mfma_kernel.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace ce {
@@ -36,14 +38,28 @@ struct Table {
 using Gen = Table<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
 static_assert(16 == kGenMaxF / 4, "one instance per k-step count");
 
+// CE_LR_MODE = 0 / 1 / 2 caps the row-loop mode below what lr_mode(N)
+// allows (experiments; optimize_lr_mfma.h)
+int lr_mode_cap() {
+    static const int cap = [] {
+        const char *m = std::getenv("CE_LR_MODE");
+        return m ? std::atoi(m) : 2;
+    }();
+    return cap;
+}
+
 template <int NKF>
 void launch_lr(const StepArgs<double> &a, hipStream_t stream) {
     const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
-    if (a.N % 16 == 0)
-        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, false>), dim3(grid), dim3(kLrBlock), 0,
+    const int mode = std::min(lr_mode(a.N), lr_mode_cap());
+    if (mode == 2)
+        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 2>), dim3(grid), dim3(kLrBlock), 0,
+                           stream, a);
+    else if (mode == 1)
+        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 1>), dim3(grid), dim3(kLrBlock), 0,
                            stream, a);
     else
-        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, true>), dim3(grid), dim3(kLrBlock), 0,
+        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 0>), dim3(grid), dim3(kLrBlock), 0,
                            stream, a);
 }
 constexpr GenFn kLrSteps[4] = {launch_lr<1>, launch_lr<2>, launch_lr<3>, launch_lr<4>};

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Step launches split over two streams (CE_SPLIT=1): parity, bench at the
+# driver's 20 steps and at 2000, graph and direct launches, pair and LR.
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out/r2o
+mkdir -p $OUT
+export TMPDIR=/tmp
+fatal() { case $1 in 0) ;; *) echo "GPU step failed (rc=$1), stopping"; exit $1;; esac; }
+CE_SPLIT=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_paths.py tests/test_gpu_dropin.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc"; grep -E "FAIL|Error" $OUT/pytest.log | head -5; tail -2 $OUT/pytest.log; fatal $rc
+run() {  # name, steps, warmup, env...
+  local name=$1 st=$2 wu=$3; shift 3
+  env "$@" timeout -k 10 120 python bench.py --steps $st --warmup $wu --no-cpu-baseline > $OUT/b_$name.log 2>&1; rc=$?; fatal $rc
+  python3 -c "import json; d=json.loads([l for l in open('$OUT/b_$name.log') if l.startswith('{')][-1]); print('$name', round(d['ms_per_step']*1e3,3), 'us/step; kernel', round(d['roofline']['kernel_ms_median']*1e3,3), d['roofline']['kernel'])"
+}
+for rep in 1 2; do
+  run pair_$rep 2000 200
+  run pairsplit_$rep 2000 200 CE_SPLIT=1
+  run pairsplitdirect_$rep 2000 200 CE_SPLIT=1 CE_MANY_DIRECT=100000
+  run lrsplit_$rep 2000 200 CE_SPLIT=1 CE_LR_MFMA=1 CE_LR_STAGE=0
+  run pair20_$rep 20 5
+  run pairsplit20_$rep 20 5 CE_SPLIT=1
+  run pairsplitdirect20_$rep 20 5 CE_SPLIT=1 CE_MANY_DIRECT=100000
+done
+echo ALL_OK

@@ -20,7 +20,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ('optimize_pair_kernel', 'optimize_step_kernel')   # the engine's step kernels
+KERNELS = ('optimize_lr_mfma_kernel', 'optimize_pair_kernel', 'optimize_step_kernel')   # the engine's step kernels
 
 
 def main():

@@ -182,7 +182,8 @@ def test_unsupported_shapes_fail_loudly():
 
 # ---------------------------------------------------------------------------
 # The two-class full-batch kernel with envs on the MFMA N dimension
-# (optimize_lr_mfma.h; CE_LR_MFMA=1) for K = 2, F <= 16, B = N in float64.
+# (optimize_lr_mfma.h; the default, CE_LR_MFMA=0 selects the register
+# kernel) for K = 2, F <= 16, B = N in float64.
 
 def _two_class(n_rows, n_features, seed):
     rs = np.random.RandomState(seed)
@@ -192,10 +193,13 @@ def _two_class(n_rows, n_features, seed):
 
 
 @pytest.mark.parametrize('n_rows,n_features,num_envs', [
-    (256, 10, 37), (200, 1, 16), (203, 13, 17), (1000, 16, 5), (4000, 4, 3), (256, 5, 1)])
+    (256, 10, 37), (200, 1, 16), (203, 13, 17), (1000, 16, 5), (4000, 4, 3), (256, 5, 1),
+    (384, 7, 21), (512, 3, 33)])
 def test_lr_mfma_kernel_matches_oracle(n_rows, n_features, num_envs):
     """Ragged row tiles (N % 16 != 0), partial 16-env groups, every k-step
-    count, many tiles per wave (the cross-entropy product folds)."""
+    count, many tiles per wave (the cross-entropy product folds), and the
+    three row-loop modes (lr_mode: 256, 512 tile pairs; 384 one unmasked
+    tile at a time; the others masked)."""
     ds = _two_class(n_rows, n_features, n_rows + n_features)
     eng = _engine(ds, num_envs, None, lr=True)
     assert eng.step_kernel == 'optimize_lr_mfma_kernel<%d>' % ((n_features + 3) // 4)
@@ -205,8 +209,8 @@ def test_lr_mfma_kernel_matches_oracle(n_rows, n_features, num_envs):
 
 
 def test_lr_mfma_agrees_with_register_kernel(lr_dataset):
-    """Same envs through the MFMA kernel (CE_LR_MFMA=1) and the default
-    two-envs-per-wave register kernel: float64 results agree to float32
+    """Same envs through the MFMA kernel and the two-envs-per-wave register
+    kernel (CE_LR_MFMA=0): float64 results agree to float32
     rounding."""
     E, T = 64, 45
     acts = np.random.RandomState(3).normal(0, 0.02, (T, E, 20)).astype(np.float32)
