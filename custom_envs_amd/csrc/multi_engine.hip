@@ -28,9 +28,10 @@ int multi_grid(int E) {
 }
 template <int P>
 void launch_multi_step(const ce::MultiArgs &a, int, hipStream_t s) {
-    // LDS stage of the observation rows: 4 waves x (64/G envs x P rows x 3H)
+    // LDS stage of the observation rows: per wave 64/G envs x P rows x 3H
     const size_t lds = a.H <= ce::kMultiStageH
-                           ? 4 * (64 / ce::Group<P>::G) * P * 3 * a.H * sizeof(float) : 0;
+                           ? ce::kMultiBlock / 64 * (64 / ce::Group<P>::G) * P * 3 * a.H * sizeof(float)
+                           : 0;
     hipLaunchKernelGGL(ce::multi_step_kernel<P>, dim3(multi_grid<P>(a.E)), dim3(ce::kMultiBlock),
                        lds, s, a);
 }

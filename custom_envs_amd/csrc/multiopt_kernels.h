@@ -38,7 +38,13 @@
 namespace ce {
 
 constexpr int kRawHist = 5;
-constexpr int kMultiBlock = 256;
+#ifndef CE_MULTI_WAVES
+#define CE_MULTI_WAVES 1
+#endif
+// One wave per workgroup: config 5's 1024 envs are 64 waves, which then
+// spread over 64 CUs instead of sharing 16 (each wave's loads are all issued
+// up front, so CU-local load throughput matters).
+constexpr int kMultiBlock = 64 * CE_MULTI_WAVES;
 constexpr int kMultiInfo = 14;     // info keys, order in include/custom_envs_amd.h
 constexpr int kMultiMaxP = 16;
 constexpr int kMultiStageH = 20;   // LDS-staged observation rows up to this H
@@ -184,7 +190,7 @@ template <int P>
 __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
 #pragma clang fp contract(off)
     constexpr int G = Group<P>::G;
-    extern __shared__ float stage[];          // [4 waves][64 / G * P * 3H] when H <= kMultiStageH
+    extern __shared__ float stage[];          // [waves][64 / G * P * 3H] when H <= kMultiStageH
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t gt = static_cast<size_t>(blockIdx.x) * kMultiBlock + threadIdx.x;
     const size_t e = gt / G;
