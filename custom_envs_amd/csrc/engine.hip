@@ -170,6 +170,9 @@ ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs
     a.accuracy = o.accuracy;
     a.episode_len = o.episode_len;
     a.diag = e->diag;
+    a.inv_B = 1.0 / static_cast<double>(e->cfg.batch_size);
+    const int P = e->cfg.n_features * e->cfg.n_classes;
+    a.p_mul = (65536 + P - 1) / P;
     return a;
 }
 

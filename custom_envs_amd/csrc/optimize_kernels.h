@@ -90,6 +90,8 @@ struct StepArgs {
     float *accuracy;
     int32_t *episode_len;
     unsigned long long *diag;   // [E][kStamps] (CE_DIAG builds only)
+    double inv_B;               // 1 / B, correctly rounded (host)
+    int p_mul;                  // ceil(65536 / P): j = (t p_mul) >> 16 = t / P for t < 2^9
 };
 
 // Diagnostic builds (-DCE_DIAG) stamp s_memtime at phase boundaries into a

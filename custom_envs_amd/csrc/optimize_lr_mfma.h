@@ -16,15 +16,23 @@
 // row (l>>4) + 4q, env l&15 -- the B operand of k-step q.
 //
 // Mapping: a workgroup owns 16 envs; its kLrWaves waves split the rows
-// (16-row tiles t = wave, wave + kLrWaves, ...).  Rows come from a
-// fragment-ordered image built once at ce_create (every MFMA operand one
-// coalesced 8-byte load per lane, no LDS staging and no barrier before the
-// math; staging the rows row-major into LDS by LDS-DMA and reading the
-// operands from there was measured slower), the W' operands
-// from the envs' state.  Each wave's partial sums
-// (gradient, log-loss, hits) meet in LDS; the epilogue -- recurrences,
-// observation, state, auto-reset (optimize.py:80-100, utils_venv.py:31) --
-// is spread over the workgroup's threads.
+// (16-row tiles t = wave, wave + kLrWaves, ...).  Forward operands come from
+// a fragment-ordered image built once at ce_create (one coalesced 8-byte
+// load per lane per k-step, no LDS staging and no barrier before the math);
+// the gradient's A operand is the same 16 x 16 tile transposed, so each
+// wave turns its forward operands around through its own LDS tile instead
+// of loading a second copy (the tile loads fell from 7 to 3 per 16 rows).
+// Each wave's partial sums (gradient; log-loss and hits already folded over
+// an env's 4 lane groups) meet in LDS behind the workgroup's ONE barrier;
+// then a "scalar" thread per env (loss, accuracy, L', reward, done) and a
+// "parameter" thread per (env, parameter) (G', W', obs) run side by side
+// (optimize.py:80-100, utils_venv.py:31 auto-reset).  Loaded state is
+// consumed before any store is issued (vmcnt counts stores too), the
+// epilogue's divisors are known at the start, so their reciprocals are
+// formed there and each quotient is 3 dependent FMAs (div_rcp).
+// Measured anatomy: 1.7 us launch floor, ~1.0 us state
+// round trip, ~2.5 us row work (softmax VALU ~1.4, f64 MFMA ~1.2: the f64
+// matrix rate equals the f64 vector rate on gfx950), ~0.7 us epilogue.
 #pragma once
 
 #include "optimize_kernels.h"
@@ -70,72 +78,143 @@ __host__ __device__ constexpr int lr_mode(int N) {
                                                           : 1;
 }
 
+// exp argument range of the signed two-class form: t = e^-u for u clamped
+// to [-700, 750] (e^700 < DBL_MAX; past either end p_y + 1e-16 and q are
+// the same float64 numbers as unclamped)
+__device__ __forceinline__ double clamp_u(double u) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(u), "v"(-700.0));
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(r), "v"(750.0));
+    return r;
+}
+
+// 1/d for any normal finite d != 0: hardware reciprocal + two Newton steps
+// (within an ulp; the residual step of div_rcp absorbs it)
+__device__ __forceinline__ double rcp_newton2(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    return fma(r, fma(-d, r, 1.0), r);
+}
+
+// a / b from rb ~ 1/b (formed off the critical path):
+// q0 = a rb, then one residual correction (Markstein) gives the correctly
+// rounded quotient, as IEEE division does, in 3 dependent operations
+__device__ __forceinline__ double div_rcp(double a, double b, double rb) {
+    const double q0 = a * rb;
+    return fma(fma(-q0, b, a), rb, q0);
+}
+
+// e^-x for 4 arguments x in [-700, 750], the 4 chains interleaved:
+// m = rint(-x log2e) by the 1.5 2^52 shifter (the integer lands in the low
+// word: no conversion instruction), r = -x - m ln2 in [-ln2/2, ln2/2],
+// Horner on kExpCoef (three-operand FMAs, as exp_neg_multi_clamped), 2^m by
+// ldexp
+__device__ __forceinline__ void exp_neg4(double (&a)[4]) {
+    constexpr double kShift = 0x1.8p52;
+    double big[4], r[4], q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        big[i] = fma(a[i], -kLog2e, kShift);
+        const double m = big[i] - kShift;
+        r[i] = fma(m, -kLn2Lo, fma(m, -kLn2Hi, -a[i]));
+        q[i] = kExpCoef[kExpTerms - 1];
+    }
+#pragma unroll
+    for (int k = kExpTerms - 2; k >= 0; --k) {
+        const double ck = kExpCoef[k];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(q[i]) : "v"(q[i]), "v"(r[i]), "v"(ck));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        a[i] = ldexp(q[i], static_cast<int>(static_cast<unsigned long long>(__double_as_longlong(big[i]))));
+}
+
+// sum of an int over lanes l, l^16, l^32, l^48 (permlane swaps)
+__device__ __forceinline__ int fold_env_lanes(int v) {
+    unsigned x = static_cast<unsigned>(v), y = x;
+    swap_halves_u32<16>(x, y);
+    x += y;
+    y = x;
+    swap_halves_u32<32>(x, y);
+    return static_cast<int>(x + y);
+}
+
 template <int NKF, int MODE>
 __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<double> a) {
     constexpr int P_MAX = 2 * kLrMaxF;
     constexpr int TD = lr_tile_doubles(NKF);
-    __shared__ double red[kLrWaves][6][kWave];          // per-wave partials
-    __shared__ double tot[6][kWave];                    // workgroup totals
+    constexpr int NT = MODE == 2 ? 2 : 1;               // row tiles in flight per wave
+    constexpr int XS = 17;                              // transpose row stride (doubles)
+    __shared__ double xt[kLrWaves][NT][16 * XS];        // per-wave X~ tile transposes
+    __shared__ double red_s[kLrWaves][4][kWave];        // per-wave gradient partials
+    __shared__ double red_l[kLrWaves][kLrEnvs];         // per-wave -log CE partials
+    __shared__ double red_h[kLrWaves][kLrEnvs];         // per-wave hit counts
     __shared__ double wsh[kLrEnvs][P_MAX];              // W' of the group's envs
-    __shared__ int wipe_sh[kLrEnvs];                    // auto-reset this step
 #ifdef CE_DIAG
     unsigned long long stamps[kStamps] = {0};
     stamps[6] = __builtin_amdgcn_s_memrealtime();
 #endif
     CE_STAMP(0);
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, h = lane >> 4;
-    const int F = a.F, P = 2 * F, N = a.N;
+    const int F = a.F, P = 2 * F, N = a.N, B = a.B, OBS = 2 * P + 1;
     const int e0 = blockIdx.x * kLrEnvs;
     const int e = e0 + c;                               // this lane's env (columns)
     const bool env_ok = e < a.E;
-    const size_t pbase = static_cast<size_t>(env_ok ? e : 0) * P;
+    // 32-bit element offsets throughout: every load / store is a uniform
+    // base (SGPRs) + a VGPR offset, no 64-bit address arithmetic
+    const unsigned pbase = static_cast<unsigned>(env_ok ? e : 0) * P;
     const double *img = reinterpret_cast<const double *>(a.data);
     const int ntiles = (N + 15) / 16;
 
-    // ---- every state load of the step issued before any is used (one
-    // memory round trip): W and the action of features 4k + h of env c
-    // (forward B operand), then the epilogue's per (env, parameter) G and
-    // W0 and per env L and the step counter
+    // ---- every state load of the step issued before any is used, ahead of
+    // the row tiles' loads (one memory round trip; waiting for the state
+    // does not wait for the tiles):
+    //  - W and the action of features 4k + h of env c (forward B operand);
+    //  - role "parameter" (thread j P + p < 16 P): G and W0 of parameter p
+    //    of env e0 + j and that env's step counter;
+    //  - role "scalar" (one thread per env of the group): L and the step
+    //    counter; spare threads past the parameter roles when there are
+    //    16 of them (F <= 15), else the p = 0 thread of each env.
     double2 wv[NKF];
-    float av0[NKF], av1[NKF];
+    float2 av[NKF];
 #pragma unroll
     for (int k = 0; k < NKF; ++k) {
         const int f = 4 * k + h;
-        const size_t i0 = pbase + (f < F ? 2 * f : 0);
+        const unsigned i0 = pbase + (f < F ? 2 * f : 0);
         wv[k] = *reinterpret_cast<const double2 *>(a.W + i0);   // 16-B aligned: P even
-        av0[k] = a.act[i0];
-        av1[k] = a.act[i0 + 1];
+        av[k] = *reinterpret_cast<const float2 *>(a.act + i0);  // 8-B aligned
     }
-    const int tid = threadIdx.x;
-    const int B = a.B;
     const int np_ = kLrEnvs * P;
-    double g_prev = 0.0, w_init = 0.0;
-    {
-        const int j = tid / P;
-        const int ee = e0 + (tid < np_ ? j : 0);
-        const size_t gi = static_cast<size_t>(ee < a.E ? ee : 0) * P + (tid < np_ ? tid - j * P : 0);
-        g_prev = a.G[gi];
-        w_init = a.W0[gi];
-    }
-    const int es = e0 + (tid < kLrEnvs ? tid : 0);
-    const double lprev = a.L[es < a.E ? es : 0];
-    const int step_prev = a.step[es < a.E ? es : 0];
+    const int pj = (tid * a.p_mul) >> 16, pp = tid - pj * P;   // tid / P, tid % P
+    const bool prole = tid < np_ && e0 + pj < a.E;
+    const unsigned gi = static_cast<unsigned>(prole ? e0 + pj : 0) * P + (prole ? pp : 0);
+    const double g_prev = a.G[gi];
+    const double w_init = a.W0[gi];
+    const int step_p = a.step[prole ? e0 + pj : 0];
+    const int sj = np_ + kLrEnvs <= kLrBlock ? tid - np_ : (tid < np_ && pp == 0 ? pj : -1);
+    const bool srole = sj >= 0 && sj < kLrEnvs && e0 + sj < a.E;
+    const unsigned es = srole ? e0 + sj : 0;
+    const double lprev = a.L[es];
+    const int step_prev = a.step[es];
 
-    // the wave's row tiles, each one's operands loaded a tile ahead
+    // the wave's row tiles, each one's forward operands loaded a tile ahead
     constexpr bool PAD = MODE == 0;
     constexpr bool FULL = MODE == 2;
-    // MFMA operands of tile t: forward A X~[16t + c][4k + h], gradient A
-    // X~[16t + h + 4q][c], labels of rows 16t + h + 4q
-    auto operands = [&](int t, double (&fv)[NKF], double (&gv)[4], int (&yv)[4], bool grad,
-                        bool labels) {
-        const double *ti = img + static_cast<size_t>(t) * TD;
+    // forward A of tile t: X~[16t + c][4k + h]; labels of rows 16t + h + 4q
+    auto operands = [&](int t, double (&fv)[NKF], int (&yv)[4], bool labels) {
+        const double *ti = img + static_cast<unsigned>(t) * TD;
+#if defined(CE_LR_EXP) && CE_LR_EXP == 4
+#pragma unroll
+        for (int k = 0; k < NKF; ++k) fv[k] = 1e-3 * (t + k + lane);   // experiment: no tile loads
+#else
 #pragma unroll
         for (int k = 0; k < NKF; ++k) fv[k] = ti[k * kWave + lane];
-        if (grad)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) gv[q] = ti[(NKF + q) * kWave + lane];
+#endif
         if (labels) {
             const int2 ya = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
             const int2 yb = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
@@ -145,13 +224,13 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
             yv[3] = yb.y;
         }
     };
-    double xf[NKF], xg[4], xf2[NKF], xg2[4];
+    double xf[NKF], xf2[NKF];
     int yl[4] = {0, 0, 0, 0}, yl2[4];
     auto load_tile = [&](int t) {
-        operands(t, xf, xg, yl, true, PAD);
-        if constexpr (FULL) operands(t + kLrWaves, xf2, xg2, yl2, true, false);   // the pair's second tile
+        operands(t, xf, yl, PAD);
+        if constexpr (FULL) operands(t + kLrWaves, xf2, yl2, false);   // the pair's second tile
     };
-    if (wave < ntiles) load_tile(wave);
+    load_tile(wave < ntiles ? wave : 0);               // unconditional: no merge-point vmcnt(0)
 
     // ---- W' = W - a (optimize.py:74-75); forward B operand: the margin
     // w'_f0 - w'_f1 of feature 4k + h for env c
@@ -160,116 +239,162 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     for (int k = 0; k < NKF; ++k) {
         const int f = 4 * k + h;
         const bool own = f < F;
-        const double w0 = wv[k].x - static_cast<double>(av0[k]);
-        const double w1 = wv[k].y - static_cast<double>(av1[k]);
+        const double w0 = wv[k].x - static_cast<double>(av[k].x);
+        const double w1 = wv[k].y - static_cast<double>(av[k].y);
         wd[k] = own ? w0 - w1 : 0.0;
         if (wave == 0 && own) {                         // kept for the epilogue
             wsh[c][2 * f] = w0;
             wsh[c][2 * f + 1] = w1;
         }
     }
+    const int cur = step_prev + 1;
+    // the epilogue's divisors are known now: their reciprocals leave the
+    // critical path (div_rcp)
+    const double dB = static_cast<double>(B), dL = lprev + 0.1;
+    double rB = a.inv_B, rL = rcp_newton2(dL);
+    const double dG = fabs(g_prev) + 1.0;
+    double rG = rcp_newton2(dG);
+    // Pin the state values and the reciprocals in registers here.  vmcnt
+    // counts stores too, so a first use of a loaded value in the epilogue
+    // would wait for the completion of every store issued before it; and
+    // left alone the compiler sinks the reciprocals into the epilogue.
+    asm volatile("" : "+v"(rB), "+v"(rL), "+v"(rG) : "v"(w_init), "v"(step_p));
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     CE_STAMP(1);
 
-    lr_d4 s = {0.0, 0.0, 0.0, 0.0};
-    double prod = 1.0, nlog = 0.0, tmax = 0.0;
+    // one gradient accumulator per tile slot: the two tiles' MFMA chains do
+    // not wait on each other (summed after the loop)
+    lr_d4 sacc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) sacc[i] = lr_d4{0.0, 0.0, 0.0, 0.0};
+    double prod = 1.0, nlog = 0.0, umin = 1.0;
     int hits = 0;
     int since = 0;
-    // two-class softmax of TwoClassModel per (row, env): t = e^-|u|, p of
-    // the larger logit 1/(1+t); q = 1 - p_y (the gradient weight).  Argmax
-    // hit = u > 0 except on a tie (t == 1), which max(t) flags for the exact
-    // pass after the loop.
+    // two-class softmax of TwoClassModel per (row, env) in its signed form:
+    // u = s_y z, t = e^-u, p_y = 1/(1+t), q = 1 - p_y = t p_y (the gradient
+    // weight) -- no per-row selects.  Argmax hit = u > 0 except on a tie
+    // (e^-|u| == 1, so |u| < 2^-52), which min |u| flags for the exact pass
+    // after the loop.
     auto softmax = [&](const lr_d4 &u, const int (&ys)[4], double (&qv)[4]) {
+#if defined(CE_LR_EXP) && CE_LR_EXP == 5
+#pragma unroll
+        for (int q = 0; q < 4; ++q) qv[q] = u[q] * 1e-3;   // experiment: no softmax
+        return;
+#endif
         double tx[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tx[q] = abs_clamp750(u[q]);
-        exp_neg_multi_clamped<4>(tx);                   // t = e^-|u|, 4 chains interleaved
+        for (int q = 0; q < 4; ++q) tx[q] = clamp_u(u[q]);
+        exp_neg4(tx);                                   // t = e^-u, 4 chains interleaved
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const double uq = u[q];
-            const double tq = tx[q];
-            const double inv = rcp_unit(1.0 + tq);
-            const double lo = tq * inv;
-            const bool neg = uq < 0.0;
+            const double inv = rcp_unit(1.0 + tx[q]);   // p_y
             const bool valid = !PAD || ys[q] >= 0;
-            qv[q] = valid ? (neg ? inv : lo) : 0.0;
-            prod *= valid ? (neg ? lo : inv) + 1e-16 : 1.0;
-            tmax = fmax(tmax, valid ? tq : 0.0);
+            qv[q] = valid ? tx[q] * inv : 0.0;
+            prod *= valid ? inv + 1e-16 : 1.0;
+            umin = fmin(umin, valid ? fabs(uq) : 1.0);
             hits += (valid && uq > 0.0) ? 1 : 0;
         }
     };
     auto forward = [&](const double (&xv)[NKF]) {
+#if defined(CE_LR_EXP) && CE_LR_EXP == 6
+        return lr_d4{xv[0] * wd[0], xv[1] * wd[1], xv[NKF - 1] * wd[0], xv[0] * wd[NKF - 1]};   // experiment: no MFMA
+#endif
         lr_d4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < NKF; ++k) u = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[k], wd[k], u, 0, 0, 0);
         return u;
     };
-    auto gradient = [&](const double (&xv)[4], const double (&qv)[4]) {
+    // gradient A operand X~[16t + h + 4q][c] is the forward operand's tile
+    // transposed: through the wave's own LDS tile (in-order LDS within a
+    // wave; no barrier).  Feature rows c >= 4 NKF read a finite stand-in:
+    // rows of S past F are never used.
+    auto put = [&](int slot, const double (&fv)[NKF]) {
+        double *x = &xt[wave][slot][0];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[q], qv[q], s, 0, 0, 0);
+        for (int k = 0; k < NKF; ++k) x[c * XS + 4 * k + h] = fv[k];
+        __builtin_amdgcn_wave_barrier();
     };
+    auto gradient = [&](int slot, const double (&qv)[4]) {
+        const double *x = &xt[wave][slot][0];
+        const int cc = c < 4 * NKF ? c : 0;
+        double gv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gv[q] = x[(h + 4 * q) * XS + cc];
+#if defined(CE_LR_EXP) && CE_LR_EXP == 6
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sacc[slot][q] = fma(gv[q], qv[q], sacc[slot][q]);   // experiment: no MFMA
+#else
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sacc[slot] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[q], qv[q], sacc[slot], 0, 0, 0);
+#endif
+        __builtin_amdgcn_wave_barrier();
+    };
+    // waves 4-7 share SIMDs with waves 0-3 and lose every VALU / matrix
+    // issue arbitration to their older partners; one static priority raise
+    // for the row work (6.17 -> 6.05 us per 4096-env launch; a stagger of
+    // their tile order instead measured 6.30, MI355X_MICROARCH.md "Two waves
+    // per SIMD" items 4 and 9)
+    if (wave >= kLrWaves / 2) __builtin_amdgcn_s_setprio(1);
 #if defined(CE_LR_EXP) && (CE_LR_EXP == 1 || CE_LR_EXP == 3)
     const int t_first = ntiles;                         // experiment: no row work
 #else
     const int t_first = wave;
 #endif
+    const int none[4] = {0, 0, 0, 0};
     if constexpr (FULL) {
-        const int none[4] = {0, 0, 0, 0};
         for (int t = t_first; t < ntiles; t += 2 * kLrWaves) {
             if (++since > 2) {                          // 16 factors in (1e-16, 1]: fold
                 nlog -= log_pos(prod);
                 prod = 1.0;
                 since = 1;
             }
-            double cf[NKF], cg[4], cf2[NKF], cg2[4];
+            double cf[NKF], cf2[NKF];
 #pragma unroll
             for (int k = 0; k < NKF; ++k) {
                 cf[k] = xf[k];
                 cf2[k] = xf2[k];
             }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                cg[q] = xg[q];
-                cg2[q] = xg2[q];
-            }
             if (t + 2 * kLrWaves < ntiles) load_tile(t + 2 * kLrWaves);
+            double qa[4], qb[4];
             const lr_d4 ua = forward(cf);
             const lr_d4 ub = forward(cf2);
-            double qa[4], qb[4];
+            put(0, cf);
+            put(1, cf2);
             softmax(ua, none, qa);
-            gradient(cg, qa);
+            gradient(0, qa);
             softmax(ub, none, qb);
-            gradient(cg2, qb);
+            gradient(1, qb);
         }
     } else {
-        const int none[4] = {0, 0, 0, 0};
         for (int t = t_first; t < ntiles; t += kLrWaves) {
             if (++since > 4) {                          // 16 factors in (1e-16, 1]: fold
                 nlog -= log_pos(prod);
                 prod = 1.0;
                 since = 1;
             }
-            double cf[NKF], cg[4];
+            double cf[NKF];
 #pragma unroll
             for (int k = 0; k < NKF; ++k) cf[k] = xf[k];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) cg[q] = xg[q];
             const int ys[4] = {yl[0], yl[1], yl[2], yl[3]};
             if (t + kLrWaves < ntiles) load_tile(t + kLrWaves);
+            const lr_d4 u = forward(cf);
+            put(0, cf);
             double qv[4];
-            softmax(forward(cf), PAD ? ys : none, qv);
-            gradient(cg, qv);
+            softmax(u, PAD ? ys : none, qv);
+            gradient(0, qv);
         }
     }
     // a tie (p0 == p1) is np.argmax's class 0: hit iff y == 0.  Only a wave
-    // that saw t == 1 re-walks its tiles (practically never: |z| < 2^-53).
-    if (__any(tmax == 1.0)) {
+    // that saw |u| < 2^-52 re-walks its tiles with the exact test e^-|u| == 1
+    // (practically never).
+    if (__any(umin < 0x1p-52)) {
         for (int t = wave; t < ntiles; t += kLrWaves) {
-            double fv[NKF], gv[4];
+            double fv[NKF];
             int ys[4];
-            operands(t, fv, gv, ys, false, true);
+            operands(t, fv, ys, true);
             const lr_d4 u = forward(fv);
             double tx[4];
 #pragma unroll
@@ -280,75 +405,70 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
                 if (ys[q] >= 0 && tx[q] == 1.0) hits += (ys[q] == 0 ? 1 : 0) - (u[q] > 0.0 ? 1 : 0);
         }
     }
-    // partials of this wave: s (features h + 4r of env c), -log of the
-    // cross-entropy factors, hits
-    red[wave][0][lane] = s[0];
-    red[wave][1][lane] = s[1];
-    red[wave][2][lane] = s[2];
-    red[wave][3][lane] = s[3];
-    red[wave][4][lane] = nlog - log_pos(prod);
-    red[wave][5][lane] = static_cast<double>(hits);
-    CE_STAMP(2);
-    __syncthreads();
-    if (wave < 6) {                                     // wave v sums value v over waves
-        double acc = 0.0;
-#pragma unroll
-        for (int w = 0; w < kLrWaves; ++w) acc += red[w][wave][lane];
-        if (wave >= 4) {                                // loss, hits: + lanes of the same env
-            acc = fold_pair<16>(acc, acc);
-            acc = fold_pair<32>(acc, acc);
-        }
-        tot[wave][lane] = acc;
+    // outputs nothing reads back in this launch, issued once the row loop
+    // has consumed its loads (vmcnt counts stores as well): the
+    // observation's weight part (wght_hist is identically 0), done and the
+    // episode length
+    const unsigned orow = static_cast<unsigned>(e0 + pj) * OBS;
+    if (prole) a.obs[orow + pp] = 0.0f;
+    if (srole) {
+        a.done[es] = cur >= a.max_steps ? 1 : 0;
+        a.episode_len[es] = cur;
     }
-    __syncthreads();
+    // partials of this wave: s (features h + 4r of env c); -log of the
+    // cross-entropy factors and the hits summed over the env's 4 lane groups
+    double lsum = nlog - log_pos(prod);
+    lsum = fold_pair<16>(lsum, lsum);
+    lsum = fold_pair<32>(lsum, lsum);
+    const double hsum = static_cast<double>(fold_env_lanes(hits));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red_s[wave][r][lane] = NT == 2 ? sacc[0][r] + sacc[NT - 1][r] : sacc[0][r];
+    if (lane < kLrEnvs) {
+        red_l[wave][lane] = lsum;
+        red_h[wave][lane] = hsum;
+    }
+    CE_STAMP(2);
+    __syncthreads();                                    // the one workgroup barrier
     CE_STAMP(3);
 
-    // ---- epilogue over the group's 16 envs, spread over the threads
+    // ---- epilogue: the scalar and the parameter roles run side by side
 #if defined(CE_LR_EXP) && (CE_LR_EXP == 2 || CE_LR_EXP == 3)
-    if (tid < kLrEnvs && e0 + tid < a.E) a.reward[e0 + tid] = static_cast<float>(tot[4][tid]);
+    if (srole) a.reward[es] = static_cast<float>(red_l[0][sj]);
     return;                                             // experiment: no epilogue
 #endif
-    // per env scalars: thread j < 16 handles env e0 + j
-    const int OBS = 2 * P + 1;
-    if (tid < kLrEnvs && e0 + tid < a.E) {
-        const int ee = e0 + tid;
-        const double loss = tot[4][tid] / B;            // lane tid holds env tid, h = 0
-        const double acc = tot[5][tid] / B;
-        const int cur = step_prev + 1;
-        const double lnew = (loss - lprev) / (lprev + 0.1);
-        const bool done = cur >= a.max_steps;
-        const bool wipe = done && a.auto_reset;
-        a.reward[ee] = static_cast<float>(-loss);
-        a.done[ee] = done ? 1 : 0;
-        a.objective[ee] = static_cast<float>(loss);     // B == N: the same numbers
-        a.accuracy[ee] = static_cast<float>(acc);
-        a.episode_len[ee] = cur;
-        a.obs[static_cast<size_t>(ee) * OBS + P] = wipe ? 0.0f : static_cast<float>(lnew);
-        a.L[ee] = wipe ? 0.0 : lnew;
-        a.step[ee] = wipe ? 0 : cur;
-        wipe_sh[tid] = wipe ? 1 : 0;
-    }
-    __syncthreads();
-    CE_STAMP(4);
-    // per (env, parameter): W', G', obs, or the auto-reset's W0 / zeros
-    if (tid < np_) {
-        const int j = tid / P, p = tid - j * P;         // env e0 + j, parameter p = 2f + col
-        const int ee = e0 + j;
-        if (ee < a.E) {
-            const bool wipe = wipe_sh[j] != 0;
-            const size_t gi = static_cast<size_t>(ee) * P + p;
-            const int f = p >> 1;
-            // S[f][env j] sits on lane j + 16 (f & 3), register f >> 2
-            const double sf = tot[f >> 2][j + 16 * (f & 3)];
-            const double g = ((p & 1) ? sf : -sf) / B;
-            const double gnew = g / (fabs(g_prev) + 1.0);
-            float *obs = a.obs + static_cast<size_t>(ee) * OBS;
-            obs[p] = 0.0f;                               // wght_hist is identically 0
-            obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(gnew);
-            a.W[gi] = wipe ? w_init : wsh[j][p];
-            a.G[gi] = wipe ? 0.0 : gnew;
+    if (srole) {
+        double lt = 0.0, ht = 0.0;
+#pragma unroll
+        for (int w = 0; w < kLrWaves; ++w) {
+            lt += red_l[w][sj];
+            ht += red_h[w][sj];
         }
+        const double loss = div_rcp(lt, dB, rB);
+        const double acc = div_rcp(ht, dB, rB);
+        const double lnew = div_rcp(loss - lprev, dL, rL);
+        const bool wipe = cur >= a.max_steps && a.auto_reset;
+        a.reward[es] = static_cast<float>(-loss);
+        a.objective[es] = static_cast<float>(loss);     // B == N: the same numbers
+        a.accuracy[es] = static_cast<float>(acc);
+        a.obs[es * OBS + P] = wipe ? 0.0f : static_cast<float>(lnew);
+        a.L[es] = wipe ? 0.0 : lnew;
+        a.step[es] = wipe ? 0 : cur;
     }
+    // per (env, parameter): W', G', obs, or the auto-reset's W0 / zeros
+    if (prole) {
+        const bool wipe = step_p + 1 >= a.max_steps && a.auto_reset;
+        const int f = pp >> 1;                          // parameter p = 2f + col
+        // S[f][env j] sits on lane j + 16 (f & 3), register f >> 2
+        double sf = 0.0;
+#pragma unroll
+        for (int w = 0; w < kLrWaves; ++w) sf += red_s[w][f >> 2][pj + 16 * (f & 3)];
+        const double g = div_rcp((pp & 1) ? sf : -sf, dB, rB);
+        const double gnew = div_rcp(g, dG, rG);
+        a.obs[orow + P + 1 + pp] = wipe ? 0.0f : static_cast<float>(gnew);
+        a.W[gi] = wipe ? w_init : wsh[pj][pp];
+        a.G[gi] = wipe ? 0.0 : gnew;
+    }
+    CE_STAMP(4);
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     CE_STAMP(5);

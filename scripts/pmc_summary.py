@@ -30,10 +30,11 @@ def main():
     p.add_argument('--precision', default='f64')
     p.add_argument('--bytes-per-env-step', type=int, default=925)
     p.add_argument('--tag', default='', help='suffix of the summary file name')
+    p.add_argument('--src', default='gpurun_out', help='directory holding prof/ and pmc/')
     args = p.parse_args()
     out_dir = os.path.join(ROOT, 'profiles')
     os.makedirs(out_dir, exist_ok=True)
-    stats = os.path.join(ROOT, 'gpurun_out', 'prof', 'run_kernel_stats.csv')
+    stats = os.path.join(ROOT, args.src, 'prof', 'run_kernel_stats.csv')
     summary = {'round': args.round, 'envs': args.envs, 'precision': args.precision}
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(out_dir, '%s_kernel_stats%s.csv' % (args.round, args.tag)))
@@ -43,7 +44,7 @@ def main():
                 summary['kernel_avg_ns'] = float(row['AverageNs'])
                 summary['kernel_calls'] = int(row['Calls'])
     counters = collections.defaultdict(list)
-    for path in sorted(glob.glob(os.path.join(ROOT, 'gpurun_out', 'pmc', 'p*',
+    for path in sorted(glob.glob(os.path.join(ROOT, args.src, 'pmc', 'p*',
                                               'run_counter_collection.csv'))):
         for row in csv.DictReader(open(path)):
             if any(k in row['Kernel_Name'] for k in KERNELS):
