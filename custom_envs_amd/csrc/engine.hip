@@ -404,11 +404,10 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         const char *force = std::getenv("CE_GENERIC");
         const bool generic = force && force[0] == '1';
         // The two-class full-batch float64 shapes (the benchmark's) run on
-        // the MFMA kernel with envs along N (optimize_lr_mfma.h): 6.30 us
-        // per 4096-env step against 6.32 for the two-envs-per-wave register
-        // kernel, 7.47 against 7.6-7.8 us per step over 20-step runs
-        // (DESIGN.md 3.9).  CE_LR_MFMA=0 (or CE_PAIR_U) selects the register
-        // kernel instead.
+        // the MFMA kernel with envs along N (optimize_lr_mfma.h): 6.09 us
+        // per 4096-env step against 6.3 for the two-envs-per-wave register
+        // kernel.  CE_LR_MFMA=0 (or CE_PAIR_U) selects the
+        // register kernel instead.
         const char *lrm = std::getenv("CE_LR_MFMA");
         lr_path = !generic && !(lrm && lrm[0] == '0') && !std::getenv("CE_PAIR_U") &&
                   cfg->precision == CE_F64 && cfg->batch_size == cfg->n_rows &&
