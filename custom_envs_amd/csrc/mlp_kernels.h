@@ -19,7 +19,7 @@
 // the info phase is a 1024 x 784 x 64 GEMM per env (MFMA-bound).  The kernel
 // is held to 256 registers so two workgroups share a CU: their phases drift
 // apart, and one env's streaming hides under another env's matrix work
-// (DESIGN.md 3.6).  The split pair mlp_train_kernel + mlp_info_kernel (same
+// (DESIGN.md 3.7).  The split pair mlp_train_kernel + mlp_info_kernel (same
 // bodies, the info pass with twice the accumulators at one wave per SIMD)
 // stays for A/B timing (CE_MLP_SPLIT=1).
 //
@@ -778,7 +778,7 @@ __device__ __forceinline__ void mlp_info_body(const MlpArgs &a, const size_t e, 
 // train phase then the info phase; at <= 256 registers two workgroups share
 // a CU, and whichever of them is in its info phase keeps the matrix pipe
 // busy while the other streams (measured 4.4-4.7 ms per 4096-env step
-// against 5.6 ms for the split pair; DESIGN.md 3.6).
+// against 5.6 ms for the split pair; DESIGN.md 3.7).
 template <bool A>
 __global__ __launch_bounds__(kMlpBlock, 2) void mlp_step_kernel(MlpArgs a) {
     __shared__ union {
