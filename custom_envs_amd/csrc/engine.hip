@@ -127,6 +127,7 @@ struct ce_engine {
     // cached hipGraph.  Measured (4096 envs, pair kernel): 20 steps 7.7 us
     // per step direct vs 8.0 graph; 100 and 2000 steps equal.
     int many_direct = 32;
+    int lr_waves = 0;         // CE_LR_WAVES: force the two-class MFMA kernel's wave count
     unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
 };
 
@@ -173,6 +174,7 @@ ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs
     a.inv_B = 1.0 / static_cast<double>(e->cfg.batch_size);
     const int P = e->cfg.n_features * e->cfg.n_classes;
     a.p_mul = (65536 + P - 1) / P;
+    a.lr_waves = e->lr_waves;
     return a;
 }
 
@@ -435,6 +437,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     e->kern = kern;
     e->mlp = mlp;
     if (const char *md = std::getenv("CE_MANY_DIRECT")) e->many_direct = std::atoi(md);
+    if (const char *lw = std::getenv("CE_LR_WAVES")) e->lr_waves = std::atoi(lw);
     // experiment switch: launch one phase only, to time each kernel alone
     if (const char *ph = std::getenv("CE_MLP_PHASES")) {
         if (std::strcmp(ph, "train") == 0) e->mlp_phases = 1;

@@ -92,6 +92,7 @@ struct StepArgs {
     unsigned long long *diag;   // [E][kStamps] (CE_DIAG builds only)
     double inv_B;               // 1 / B, correctly rounded (host)
     int p_mul;                  // ceil(65536 / P): j = (t p_mul) >> 16 = t / P for t < 2^9
+    int lr_waves;               // two-class MFMA kernel: 0 = pick per launch, 4 / 8 = forced
 };
 
 // Diagnostic builds (-DCE_DIAG) stamp s_memtime at phase boundaries into a

@@ -15,8 +15,8 @@
 // is the forward's C registers as they stand: f64 C register q of lane l is
 // row (l>>4) + 4q, env l&15 -- the B operand of k-step q.
 //
-// Mapping: a workgroup owns 16 envs; its kLrWaves waves split the rows
-// (16-row tiles t = wave, wave + kLrWaves, ...).  Forward operands come from
+// Mapping: a workgroup owns 16 envs; its W waves split the rows (16-row
+// tiles t = wave, wave + W, ...).  Forward operands come from
 // a fragment-ordered image built once at ce_create (one coalesced 8-byte
 // load per lane per k-step, no LDS staging and no barrier before the math);
 // the gradient's A operand is the same 16 x 16 tile transposed, so each
@@ -42,14 +42,15 @@ namespace ce {
 typedef double lr_d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
-#ifndef CE_LR_WAVES
-#define CE_LR_WAVES 8
-#endif
-constexpr int kLrWaves = CE_LR_WAVES;          // waves per workgroup (row split)
-constexpr int kLrBlock = kWave * kLrWaves;
 constexpr int kLrMaxF = 16;
-
-static_assert(kLrEnvs * 2 * kLrMaxF <= kLrBlock, "one epilogue thread per (env, parameter)");
+// Waves per workgroup W (the row split) is a template parameter: 8 waves
+// (2 per SIMD, 2 tiles each) or 4 waves (1 per SIMD, 4 tiles per group,
+// software-pipelined); lr_waves picks per launch (optimize_mfma.hip).
+template <int W>
+struct LrShape {
+    static constexpr int kBlock = kWave * W;
+    static constexpr int kParamSlots = (kLrEnvs * 2 * kLrMaxF + kBlock - 1) / kBlock;   // (env, parameter) roles per thread
+};
 
 __host__ __device__ constexpr bool lr_mfma_shape(int F, int K) { return K == 2 && F <= kLrMaxF; }
 __host__ __device__ constexpr int lr_nkf(int F) { return (F + 3) / 4; }
@@ -67,15 +68,16 @@ __host__ __device__ constexpr int lr_tile_doubles(int nkf) { return (nkf + 4 + 2
 // MODE (lr_mode): 0 = one tile at a time, padding rows (label -1) masked
 // out of every statistic; 1 = N a multiple of 16 and every wave owning the
 // same number of tiles, so the row loop reads no labels (the sign-folded
-// rows carry y); 2 = as 1 with an even number of tiles per wave, run two at
-// a time: both forward MFMA chains first, then softmax A, gradient MFMAs A,
-// softmax B, gradient MFMAs B, so the matrix pipe works through one tile's
-// MFMAs while the VALU does the other's softmax (f64 MFMA and f64 VALU have
-// the same rate on gfx950; only the overlap gains).
-__host__ __device__ constexpr int lr_mode(int N) {
-    return N % 16 != 0 || ((N + 15) / 16) % kLrWaves != 0 ? 0
-           : ((N + 15) / 16) % (2 * kLrWaves) == 0      ? 2
-                                                          : 1;
+// rows carry y); 2 / 3 = as 1 with the wave's tiles taken 2 / 4 at a time:
+// all forward MFMA chains of the group first, then per tile softmax and
+// gradient MFMAs, so the matrix pipe works through one tile's MFMAs while
+// the VALU does another's softmax (f64 MFMA and f64 VALU have the same rate
+// on gfx950; only the overlap gains).
+__host__ __device__ constexpr int lr_mode(int N, int W) {
+    return N % 16 != 0 || ((N + 15) / 16) % W != 0 ? 0
+           : ((N + 15) / 16) % (4 * W) == 0 && W <= 4 ? 3
+           : ((N + 15) / 16) % (2 * W) == 0           ? 2
+                                                      : 1;
 }
 
 // exp argument range of the signed two-class form: t = e^-u for u clamped
@@ -104,16 +106,17 @@ __device__ __forceinline__ double div_rcp(double a, double b, double rb) {
     return fma(fma(-q0, b, a), rb, q0);
 }
 
-// e^-x for 4 arguments x in [-700, 750], the 4 chains interleaved:
+// e^-x for Q arguments x in [-700, 750], the Q chains interleaved:
 // m = rint(-x log2e) by the 1.5 2^52 shifter (the integer lands in the low
 // word: no conversion instruction), r = -x - m ln2 in [-ln2/2, ln2/2],
 // Horner on kExpCoef (three-operand FMAs, as exp_neg_multi_clamped), 2^m by
 // ldexp
-__device__ __forceinline__ void exp_neg4(double (&a)[4]) {
+template <int Q>
+__device__ __forceinline__ void exp_neg_q(double (&a)[Q]) {
     constexpr double kShift = 0x1.8p52;
-    double big[4], r[4], q[4];
+    double big[Q], r[Q], q[Q];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < Q; ++i) {
         big[i] = fma(a[i], -kLog2e, kShift);
         const double m = big[i] - kShift;
         r[i] = fma(m, -kLn2Lo, fma(m, -kLn2Hi, -a[i]));
@@ -123,11 +126,11 @@ __device__ __forceinline__ void exp_neg4(double (&a)[4]) {
     for (int k = kExpTerms - 2; k >= 0; --k) {
         const double ck = kExpCoef[k];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < Q; ++i)
             asm("v_fma_f64 %0, %1, %2, %3" : "=v"(q[i]) : "v"(q[i]), "v"(r[i]), "v"(ck));
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < Q; ++i)
         a[i] = ldexp(q[i], static_cast<int>(static_cast<unsigned long long>(__double_as_longlong(big[i]))));
 }
 
@@ -141,11 +144,14 @@ __device__ __forceinline__ int fold_env_lanes(int v) {
     return static_cast<int>(x + y);
 }
 
-template <int NKF, int MODE>
-__global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<double> a) {
+template <int NKF, int MODE, int W>
+__global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(StepArgs<double> a) {
+    constexpr int kLrWaves = W;
+    constexpr int kLrBlock = LrShape<W>::kBlock;
     constexpr int P_MAX = 2 * kLrMaxF;
     constexpr int TD = lr_tile_doubles(NKF);
-    constexpr int NT = MODE == 2 ? 2 : 1;               // row tiles in flight per wave
+    constexpr int NT = MODE == 3 ? 4 : MODE == 2 ? 2 : 1;   // row tiles per group
+    constexpr int PR = LrShape<W>::kParamSlots;
     constexpr int XS = 17;                              // transpose row stride (doubles)
     __shared__ double xt[kLrWaves][NT][16 * XS];        // per-wave X~ tile transposes
     __shared__ double red_s[kLrWaves][4][kWave];        // per-wave gradient partials
@@ -175,11 +181,10 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     // the row tiles' loads (one memory round trip; waiting for the state
     // does not wait for the tiles):
     //  - W and the action of features 4k + h of env c (forward B operand);
-    //  - role "parameter" (thread j P + p < 16 P): G and W0 of parameter p
-    //    of env e0 + j and that env's step counter;
-    //  - role "scalar" (one thread per env of the group): L and the step
-    //    counter; spare threads past the parameter roles when there are
-    //    16 of them (F <= 15), else the p = 0 thread of each env.
+    //  - role "parameter" (index i = j P + p < 16 P, i = tid + r kLrBlock):
+    //    G and W0 of parameter p of env e0 + j and that env's step counter;
+    //  - role "scalar" (the last 16 threads, one per env of the group): L
+    //    and the step counter.
     double2 wv[NKF];
     float2 av[NKF];
 #pragma unroll
@@ -190,31 +195,34 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
         av[k] = *reinterpret_cast<const float2 *>(a.act + i0);  // 8-B aligned
     }
     const int np_ = kLrEnvs * P;
-    const int pj = (tid * a.p_mul) >> 16, pp = tid - pj * P;   // tid / P, tid % P
-    const bool prole = tid < np_ && e0 + pj < a.E;
-    const unsigned gi = static_cast<unsigned>(prole ? e0 + pj : 0) * P + (prole ? pp : 0);
-    const double g_prev = a.G[gi];
-    const double w_init = a.W0[gi];
-    const int step_p = a.step[prole ? e0 + pj : 0];
-    const int sj = np_ + kLrEnvs <= kLrBlock ? tid - np_ : (tid < np_ && pp == 0 ? pj : -1);
-    const bool srole = sj >= 0 && sj < kLrEnvs && e0 + sj < a.E;
+    int pj[PR], pp[PR], step_p[PR];
+    bool prole[PR];
+    unsigned gi[PR];
+    double g_prev[PR], w_init[PR];
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+        const int i = tid + r * kLrBlock;
+        pj[r] = (i * a.p_mul) >> 16;                    // i / P, exact for i < 2^9
+        pp[r] = i - pj[r] * P;
+        prole[r] = i < np_ && e0 + pj[r] < a.E;
+        gi[r] = static_cast<unsigned>(prole[r] ? e0 + pj[r] : 0) * P + (prole[r] ? pp[r] : 0);
+        g_prev[r] = a.G[gi[r]];
+        w_init[r] = a.W0[gi[r]];
+        step_p[r] = a.step[prole[r] ? e0 + pj[r] : 0];
+    }
+    const int sj = tid - (kLrBlock - kLrEnvs);
+    const bool srole = sj >= 0 && e0 + sj < a.E;
     const unsigned es = srole ? e0 + sj : 0;
     const double lprev = a.L[es];
     const int step_prev = a.step[es];
 
-    // the wave's row tiles, each one's forward operands loaded a tile ahead
+    // the wave's row tiles, each group's forward operands loaded a group ahead
     constexpr bool PAD = MODE == 0;
-    constexpr bool FULL = MODE == 2;
     // forward A of tile t: X~[16t + c][4k + h]; labels of rows 16t + h + 4q
     auto operands = [&](int t, double (&fv)[NKF], int (&yv)[4], bool labels) {
         const double *ti = img + static_cast<unsigned>(t) * TD;
-#if defined(CE_LR_EXP) && CE_LR_EXP == 4
-#pragma unroll
-        for (int k = 0; k < NKF; ++k) fv[k] = 1e-3 * (t + k + lane);   // experiment: no tile loads
-#else
 #pragma unroll
         for (int k = 0; k < NKF; ++k) fv[k] = ti[k * kWave + lane];
-#endif
         if (labels) {
             const int2 ya = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
             const int2 yb = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
@@ -224,13 +232,13 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
             yv[3] = yb.y;
         }
     };
-    double xf[NKF], xf2[NKF];
-    int yl[4] = {0, 0, 0, 0}, yl2[4];
-    auto load_tile = [&](int t) {
-        operands(t, xf, yl, PAD);
-        if constexpr (FULL) operands(t + kLrWaves, xf2, yl2, false);   // the pair's second tile
+    double xf[NT][NKF];
+    int yl[NT][4] = {};
+    auto load_group = [&](int t) {                      // tiles t, t + kLrWaves, ...
+#pragma unroll
+        for (int i = 0; i < NT; ++i) operands(t + i * kLrWaves, xf[i], yl[i], PAD && i == 0);
     };
-    load_tile(wave < ntiles ? wave : 0);               // unconditional: no merge-point vmcnt(0)
+    load_group(wave < ntiles ? wave : 0);              // unconditional: no merge-point vmcnt(0)
 
     // ---- W' = W - a (optimize.py:74-75); forward B operand: the margin
     // w'_f0 - w'_f1 of feature 4k + h for env c
@@ -252,19 +260,24 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     // critical path (div_rcp)
     const double dB = static_cast<double>(B), dL = lprev + 0.1;
     double rB = a.inv_B, rL = rcp_newton2(dL);
-    const double dG = fabs(g_prev) + 1.0;
-    double rG = rcp_newton2(dG);
-    // Pin the state values and the reciprocals in registers here.  vmcnt
-    // counts stores too, so a first use of a loaded value in the epilogue
-    // would wait for the completion of every store issued before it; and
-    // left alone the compiler sinks the reciprocals into the epilogue.
-    asm volatile("" : "+v"(rB), "+v"(rL), "+v"(rG) : "v"(w_init), "v"(step_p));
+    double rG[PR];
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+        rG[r] = rcp_newton2(fabs(g_prev[r]) + 1.0);
+        // Pin the state values and the reciprocals in registers here.  vmcnt
+        // counts stores too, so a first use of a loaded value in the
+        // epilogue would wait for the completion of every store issued
+        // before it; and left alone the compiler sinks the reciprocals into
+        // the epilogue.
+        asm volatile("" : "+v"(rG[r]) : "v"(w_init[r]), "v"(step_p[r]));
+    }
+    asm volatile("" : "+v"(rB), "+v"(rL));
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     CE_STAMP(1);
 
-    // one gradient accumulator per tile slot: the two tiles' MFMA chains do
+    // one gradient accumulator per tile of a group: the tiles' MFMA chains do
     // not wait on each other (summed after the loop)
     lr_d4 sacc[NT];
 #pragma unroll
@@ -277,31 +290,31 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     // weight) -- no per-row selects.  Argmax hit = u > 0 except on a tie
     // (e^-|u| == 1, so |u| < 2^-52), which min |u| flags for the exact pass
     // after the loop.
+    // QC exp chains at a time: 4 with 1-2 waves per SIMD (the wave's own
+    // chains cover the f64 latency), 2 at 4 waves per SIMD (the other waves
+    // cover it, and the 128-register budget has no room for 4)
+    constexpr int QC = W >= 16 ? 2 : 4;
     auto softmax = [&](const lr_d4 &u, const int (&ys)[4], double (&qv)[4]) {
-#if defined(CE_LR_EXP) && CE_LR_EXP == 5
 #pragma unroll
-        for (int q = 0; q < 4; ++q) qv[q] = u[q] * 1e-3;   // experiment: no softmax
-        return;
-#endif
-        double tx[4];
+        for (int q0 = 0; q0 < 4; q0 += QC) {
+            double tx[QC];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tx[q] = clamp_u(u[q]);
-        exp_neg4(tx);                                   // t = e^-u, 4 chains interleaved
+            for (int i = 0; i < QC; ++i) tx[i] = clamp_u(u[q0 + i]);
+            exp_neg_q<QC>(tx);                          // t = e^-u
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const double uq = u[q];
-            const double inv = rcp_unit(1.0 + tx[q]);   // p_y
-            const bool valid = !PAD || ys[q] >= 0;
-            qv[q] = valid ? tx[q] * inv : 0.0;
-            prod *= valid ? inv + 1e-16 : 1.0;
-            umin = fmin(umin, valid ? fabs(uq) : 1.0);
-            hits += (valid && uq > 0.0) ? 1 : 0;
+            for (int i = 0; i < QC; ++i) {
+                const int q = q0 + i;
+                const double uq = u[q];
+                const double inv = rcp_unit(1.0 + tx[i]);   // p_y
+                const bool valid = !PAD || ys[q] >= 0;
+                qv[q] = valid ? tx[i] * inv : 0.0;
+                prod *= valid ? inv + 1e-16 : 1.0;
+                umin = fmin(umin, valid ? fabs(uq) : 1.0);
+                hits += (valid && uq > 0.0) ? 1 : 0;
+            }
         }
     };
     auto forward = [&](const double (&xv)[NKF]) {
-#if defined(CE_LR_EXP) && CE_LR_EXP == 6
-        return lr_d4{xv[0] * wd[0], xv[1] * wd[1], xv[NKF - 1] * wd[0], xv[0] * wd[NKF - 1]};   // experiment: no MFMA
-#endif
         lr_d4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < NKF; ++k) u = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[k], wd[k], u, 0, 0, 0);
@@ -323,68 +336,55 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
         double gv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) gv[q] = x[(h + 4 * q) * XS + cc];
-#if defined(CE_LR_EXP) && CE_LR_EXP == 6
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sacc[slot][q] = fma(gv[q], qv[q], sacc[slot][q]);   // experiment: no MFMA
-#else
 #pragma unroll
         for (int q = 0; q < 4; ++q) sacc[slot] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[q], qv[q], sacc[slot], 0, 0, 0);
-#endif
         __builtin_amdgcn_wave_barrier();
     };
-    // waves 4-7 share SIMDs with waves 0-3 and lose every VALU / matrix
-    // issue arbitration to their older partners; one static priority raise
-    // for the row work (6.17 -> 6.05 us per 4096-env launch; a stagger of
-    // their tile order instead measured 6.30, MI355X_MICROARCH.md "Two waves
-    // per SIMD" items 4 and 9)
-    if (wave >= kLrWaves / 2) __builtin_amdgcn_s_setprio(1);
+    // With two waves per SIMD, waves kLrWaves/2.. share SIMDs with the
+    // older half and lose every VALU / matrix issue arbitration; one static
+    // priority raise for the row work (6.17 -> 6.05 us per 4096-env launch
+    // at 8 waves; a stagger of their tile order instead measured 6.30,
+    // MI355X_MICROARCH.md "Two waves per SIMD" items 4 and 9)
+    if (kLrWaves == 8 && wave >= kLrWaves / 2) __builtin_amdgcn_s_setprio(1);
 #if defined(CE_LR_EXP) && (CE_LR_EXP == 1 || CE_LR_EXP == 3)
     const int t_first = ntiles;                         // experiment: no row work
 #else
     const int t_first = wave;
 #endif
     const int none[4] = {0, 0, 0, 0};
-    if constexpr (FULL) {
-        for (int t = t_first; t < ntiles; t += 2 * kLrWaves) {
-            if (++since > 2) {                          // 16 factors in (1e-16, 1]: fold
-                nlog -= log_pos(prod);
-                prod = 1.0;
-                since = 1;
-            }
-            double cf[NKF], cf2[NKF];
-#pragma unroll
-            for (int k = 0; k < NKF; ++k) {
-                cf[k] = xf[k];
-                cf2[k] = xf2[k];
-            }
-            if (t + 2 * kLrWaves < ntiles) load_tile(t + 2 * kLrWaves);
-            double qa[4], qb[4];
-            const lr_d4 ua = forward(cf);
-            const lr_d4 ub = forward(cf2);
-            put(0, cf);
-            put(1, cf2);
-            softmax(ua, none, qa);
-            gradient(0, qa);
-            softmax(ub, none, qb);
-            gradient(1, qb);
+    for (int t = t_first; t < ntiles; t += NT * kLrWaves) {
+        since += NT;
+        if (since > 4) {                                // 16 factors in (1e-16, 1]: fold
+            nlog -= log_pos(prod);
+            prod = 1.0;
+            since = NT;
         }
-    } else {
-        for (int t = t_first; t < ntiles; t += kLrWaves) {
-            if (++since > 4) {                          // 16 factors in (1e-16, 1]: fold
-                nlog -= log_pos(prod);
-                prod = 1.0;
-                since = 1;
-            }
-            double cf[NKF];
+        // 1-2 waves per SIMD: the next group's operands load while this
+        // one computes; 4 waves per SIMD: the other waves cover the load,
+        // and the registers of a second copy are not there
+        if constexpr (W >= 16)
+            if (t != t_first) load_group(t);
+        double cf[NT][NKF];
+        int ys[NT][4];
 #pragma unroll
-            for (int k = 0; k < NKF; ++k) cf[k] = xf[k];
-            const int ys[4] = {yl[0], yl[1], yl[2], yl[3]};
-            if (t + kLrWaves < ntiles) load_tile(t + kLrWaves);
-            const lr_d4 u = forward(cf);
-            put(0, cf);
+        for (int i = 0; i < NT; ++i) {
+#pragma unroll
+            for (int k = 0; k < NKF; ++k) cf[i][k] = xf[i][k];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ys[i][q] = yl[i][q];
+        }
+        if constexpr (W < 16)
+            if (t + NT * kLrWaves < ntiles) load_group(t + NT * kLrWaves);
+        lr_d4 u[NT];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) u[i] = forward(cf[i]);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) put(i, cf[i]);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
             double qv[4];
-            softmax(u, PAD ? ys : none, qv);
-            gradient(0, qv);
+            softmax(u[i], PAD ? ys[i] : none, qv);
+            gradient(i, qv);
         }
     }
     // a tie (p0 == p1) is np.argmax's class 0: hit iff y == 0.  Only a wave
@@ -393,24 +393,25 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     if (__any(umin < 0x1p-52)) {
         for (int t = wave; t < ntiles; t += kLrWaves) {
             double fv[NKF];
-            int ys[4];
-            operands(t, fv, ys, true);
-            const lr_d4 u = forward(fv);
+            int yv[4];
+            operands(t, fv, yv, true);
+            const lr_d4 uu = forward(fv);
             double tx[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) tx[q] = abs_clamp750(u[q]);
+            for (int q = 0; q < 4; ++q) tx[q] = abs_clamp750(uu[q]);
             exp_neg_multi_clamped<4>(tx);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                if (ys[q] >= 0 && tx[q] == 1.0) hits += (ys[q] == 0 ? 1 : 0) - (u[q] > 0.0 ? 1 : 0);
+                if (yv[q] >= 0 && tx[q] == 1.0) hits += (yv[q] == 0 ? 1 : 0) - (uu[q] > 0.0 ? 1 : 0);
         }
     }
     // outputs nothing reads back in this launch, issued once the row loop
     // has consumed its loads (vmcnt counts stores as well): the
     // observation's weight part (wght_hist is identically 0), done and the
     // episode length
-    const unsigned orow = static_cast<unsigned>(e0 + pj) * OBS;
-    if (prole) a.obs[orow + pp] = 0.0f;
+#pragma unroll
+    for (int r = 0; r < PR; ++r)
+        if (prole[r]) a.obs[static_cast<unsigned>(e0 + pj[r]) * OBS + pp[r]] = 0.0f;
     if (srole) {
         a.done[es] = cur >= a.max_steps ? 1 : 0;
         a.episode_len[es] = cur;
@@ -422,7 +423,12 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
     lsum = fold_pair<32>(lsum, lsum);
     const double hsum = static_cast<double>(fold_env_lanes(hits));
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red_s[wave][r][lane] = NT == 2 ? sacc[0][r] + sacc[NT - 1][r] : sacc[0][r];
+    for (int r = 0; r < 4; ++r) {
+        double v = sacc[0][r];
+#pragma unroll
+        for (int i = 1; i < NT; ++i) v += sacc[i][r];
+        red_s[wave][r][lane] = v;
+    }
     if (lane < kLrEnvs) {
         red_l[wave][lane] = lsum;
         red_h[wave][lane] = hsum;
@@ -455,18 +461,21 @@ __global__ __launch_bounds__(kLrBlock) void optimize_lr_mfma_kernel(StepArgs<dou
         a.step[es] = wipe ? 0 : cur;
     }
     // per (env, parameter): W', G', obs, or the auto-reset's W0 / zeros
-    if (prole) {
-        const bool wipe = step_p + 1 >= a.max_steps && a.auto_reset;
-        const int f = pp >> 1;                          // parameter p = 2f + col
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+        if (!prole[r]) continue;
+        const bool wipe = step_p[r] + 1 >= a.max_steps && a.auto_reset;
+        const int f = pp[r] >> 1;                       // parameter p = 2f + col
         // S[f][env j] sits on lane j + 16 (f & 3), register f >> 2
         double sf = 0.0;
 #pragma unroll
-        for (int w = 0; w < kLrWaves; ++w) sf += red_s[w][f >> 2][pj + 16 * (f & 3)];
-        const double g = div_rcp((pp & 1) ? sf : -sf, dB, rB);
-        const double gnew = div_rcp(g, dG, rG);
-        a.obs[orow + P + 1 + pp] = wipe ? 0.0f : static_cast<float>(gnew);
-        a.W[gi] = wipe ? w_init : wsh[pj][pp];
-        a.G[gi] = wipe ? 0.0 : gnew;
+        for (int w = 0; w < kLrWaves; ++w) sf += red_s[w][f >> 2][pj[r] + 16 * (f & 3)];
+        const double g = div_rcp((pp[r] & 1) ? sf : -sf, dB, rB);
+        const double gnew = div_rcp(g, fabs(g_prev[r]) + 1.0, rG[r]);
+        a.obs[static_cast<unsigned>(e0 + pj[r]) * OBS + P + 1 + pp[r]] =
+            wipe ? 0.0f : static_cast<float>(gnew);
+        a.W[gi[r]] = wipe ? w_init[r] : wsh[pj[r]][pp[r]];
+        a.G[gi[r]] = wipe ? 0.0 : gnew;
     }
     CE_STAMP(4);
 #ifdef CE_DIAG

@@ -38,29 +38,54 @@ struct Table {
 using Gen = Table<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
 static_assert(16 == kGenMaxF / 4, "one instance per k-step count");
 
-// CE_LR_MODE = 0 / 1 / 2 caps the row-loop mode below what lr_mode(N)
+// CE_LR_MODE = 0 / 1 / 2 / 3 caps the row-loop mode below what lr_mode(N)
 // allows (experiments; optimize_lr_mfma.h)
 int lr_mode_cap() {
     static const int cap = [] {
         const char *m = std::getenv("CE_LR_MODE");
-        return m ? std::atoi(m) : 2;
+        return m ? std::atoi(m) : 3;
     }();
     return cap;
 }
 
+template <int NKF, int W>
+void launch_lr_w(const StepArgs<double> &a, hipStream_t stream) {
+    const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
+    const dim3 block(LrShape<W>::kBlock);
+    const int mode = std::min(lr_mode(a.N, W), lr_mode_cap());
+    if constexpr (W <= 4) {
+        if (mode == 3) {
+            hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 3, W>), dim3(grid), block, 0, stream, a);
+            return;
+        }
+    }
+    if constexpr (W <= 8) {   // 16 waves take their tiles one at a time (128 registers)
+        if (mode == 2) {
+            hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 2, W>), dim3(grid), block, 0, stream, a);
+            return;
+        }
+    }
+    if (mode >= 1)
+        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 1, W>), dim3(grid), block, 0, stream, a);
+    else
+        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 0, W>), dim3(grid), block, 0, stream, a);
+}
+
+// Wave count: 4 waves per workgroup (one per SIMD, tiles 4 at a time,
+// software-pipelined) when the grid fills the chip and every wave gets
+// whole groups of 4 tiles: 5.95 us per 4096-env launch at 256 x 10, against
+// 6.06 at 8 waves and 7.0 at 16 (one tile per wave, 4 waves per SIMD: its
+// row phase is 2.5x cheaper per tile, but its waves start up to 3.3 us
+// apart).  Otherwise 8 waves, which halve each wave's rows
+// for small grids.  a.lr_waves = 4, 8 or 16 (CE_LR_WAVES at ce_create)
+// forces one.
 template <int NKF>
 void launch_lr(const StepArgs<double> &a, hipStream_t stream) {
-    const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
-    const int mode = std::min(lr_mode(a.N), lr_mode_cap());
-    if (mode == 2)
-        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 2>), dim3(grid), dim3(kLrBlock), 0,
-                           stream, a);
-    else if (mode == 1)
-        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 1>), dim3(grid), dim3(kLrBlock), 0,
-                           stream, a);
-    else
-        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 0>), dim3(grid), dim3(kLrBlock), 0,
-                           stream, a);
+    const int groups = (a.E + kLrEnvs - 1) / kLrEnvs;
+    const int w = a.lr_waves ? a.lr_waves : groups >= 256 && lr_mode(a.N, 4) == 3 ? 4 : 8;
+    if (w == 16) launch_lr_w<NKF, 16>(a, stream);
+    else if (w == 4) launch_lr_w<NKF, 4>(a, stream);
+    else launch_lr_w<NKF, 8>(a, stream);
 }
 constexpr GenFn kLrSteps[4] = {launch_lr<1>, launch_lr<2>, launch_lr<3>, launch_lr<4>};
 

@@ -60,7 +60,7 @@ def main():
     names = ['stage+barrier', 'state loads+bcast', 'row loop', 'reduce+info', 'epilogue']
     if 'lr_mfma' in eng.step_kernel:
         # optimize_lr_mfma_kernel: one row per wave (16 envs x 8 waves per workgroup)
-        st = st[:(E + 15) // 16 * 8]
+        st = st[st[:, 0] != 0]                      # rows = workgroups x waves (4, 8 or 16)
         names = ['W + first tile loads', 'row tiles', 'partials meet', 'scalar epilogue',
                  'param epilogue + drain']
     if 'mlp' in eng.step_kernel:

@@ -24,9 +24,10 @@ def _need_gpu():
         pytest.fail('GPU tests need a ROCm device (run under gpurun)')
 
 
-def _engine(dataset, num_envs, batch_size=None, generic=False, lr=False, **kw):
+def _engine(dataset, num_envs, batch_size=None, generic=False, lr=False, lr_waves=0, **kw):
     from custom_envs_amd.engine import OptimizeEngine
-    flags = {'CE_GENERIC': '1' if generic else '0', 'CE_LR_MFMA': '1' if lr else '0'}
+    flags = {'CE_GENERIC': '1' if generic else '0', 'CE_LR_MFMA': '1' if lr else '0',
+             'CE_LR_WAVES': str(lr_waves)}
     old = {k: os.environ.get(k) for k in flags}
     os.environ.update(flags)
     try:
@@ -192,16 +193,19 @@ def _two_class(n_rows, n_features, seed):
     return x, np.eye(2)[y]
 
 
+@pytest.mark.parametrize('lr_waves', [8, 4, 16])
 @pytest.mark.parametrize('n_rows,n_features,num_envs', [
     (256, 10, 37), (200, 1, 16), (203, 13, 17), (1000, 16, 5), (4000, 4, 3), (256, 5, 1),
-    (384, 7, 21), (512, 3, 33)])
-def test_lr_mfma_kernel_matches_oracle(n_rows, n_features, num_envs):
+    (384, 7, 21), (512, 3, 33), (1024, 10, 18)])
+def test_lr_mfma_kernel_matches_oracle(n_rows, n_features, num_envs, lr_waves):
     """Ragged row tiles (N % 16 != 0), partial 16-env groups, every k-step
     count, many tiles per wave (the cross-entropy product folds), and the
-    three row-loop modes (lr_mode: 256, 512 tile pairs; 384 one unmasked
-    tile at a time; the others masked)."""
+    four row-loop modes (lr_mode: 8 waves -- 256, 512, 1024 tile pairs, 384
+    one unmasked tile at a time, the others masked; 4 waves -- 256, 1024
+    groups of 4 tiles, 384 pairs; 16 waves -- one tile at a time), at every
+    wave count (4 waves: two (env, parameter) roles per thread)."""
     ds = _two_class(n_rows, n_features, n_rows + n_features)
-    eng = _engine(ds, num_envs, None, lr=True)
+    eng = _engine(ds, num_envs, None, lr=True, lr_waves=lr_waves)
     assert eng.step_kernel == 'optimize_lr_mfma_kernel<%d>' % ((n_features + 3) // 4)
     envs = sorted({0, num_envs // 2, num_envs - 1})
     _check(ds, None, eng, envs, 43)
