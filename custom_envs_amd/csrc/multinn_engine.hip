@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -33,6 +34,8 @@ struct ce_nn_engine {
     double *part_u = nullptr, *part_c = nullptr;
     int32_t *step = nullptr, *cursor = nullptr, *order = nullptr, *order_sel = nullptr;
     int32_t *reset_perm = nullptr, *epoch_perm = nullptr, *agent_row = nullptr;
+    int32_t *row_agent = nullptr;
+    bool agent_order = false;   // CE_NN_AGENT=agent: nn_agent_kernel (agent order) instead of rows
     float *d_act = nullptr, *h_act = nullptr;
     size_t off[5] = {0};
     size_t out_bytes = 0;
@@ -80,11 +83,15 @@ bool complete(const ce_multi_outputs *o) {
 // one step's five launches; the ping-pong pairs swap afterwards
 void launch_step(ce_nn_engine *e, const float *act, const ce_multi_outputs &o, hipStream_t s) {
     const ce::NnArgs a = make_args(e, act, o);
-    const size_t stage = static_cast<size_t>(ce::kNnChunk) * 3 * a.H * sizeof(float);
+    const size_t stage = (static_cast<size_t>(ce::kNnChunk) * 3 * a.H + 4) * sizeof(float);
     hipLaunchKernelGGL(ce::nn_grad_kernel, dim3(a.E), dim3(ce::kNnBlock), a.lds_bytes, s, a);
     hipLaunchKernelGGL(ce::nn_update_kernel, dim3(a.nchunk_u, a.E), dim3(ce::kNnChunk), 0, s, a);
     hipLaunchKernelGGL(ce::nn_step_kernel, dim3(a.E), dim3(ce::kNnBlock), a.lds_bytes, s, a);
-    hipLaunchKernelGGL(ce::nn_agent_kernel, dim3(a.nchunk, a.E), dim3(ce::kNnChunk), stage, s, a);
+    if (e->agent_order)
+        hipLaunchKernelGGL(ce::nn_agent_kernel, dim3(a.nchunk, a.E), dim3(ce::kNnChunk), stage, s, a);
+    else
+        hipLaunchKernelGGL(ce::nn_agent_rows_kernel, dim3(a.nchunk, a.E), dim3(ce::kNnChunk), stage, s,
+                           a);
     hipLaunchKernelGGL(ce::nn_finalize_kernel, dim3(a.E), dim3(ce::kNnChunk), 0, s, a);
     e->parity ^= 1;
 }
@@ -255,6 +262,7 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     CE_TRY(hipMalloc(&e->reset_perm, E * N * sizeof(int32_t)));
     CE_TRY(hipMalloc(&e->epoch_perm, E * N * sizeof(int32_t)));
     CE_TRY(hipMalloc(&e->agent_row, P * sizeof(int32_t)));
+    CE_TRY(hipMalloc(&e->row_agent, P * sizeof(int32_t)));
     CE_TRY(hipMalloc(&e->d_act, E * P * sizeof(float)));
     CE_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_act), E * P * sizeof(float)));
     CE_TRY(hipMemset(e->step, 0, E * sizeof(int32_t)));
@@ -278,6 +286,7 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
                   [&](int32_t x, int32_t y) { return names[x] < names[y]; });
         for (long r = 0; r < P; ++r) row[order[r]] = static_cast<int32_t>(r);
         CE_TRY(hipMemcpy(e->agent_row, row.data(), P * sizeof(int32_t), hipMemcpyHostToDevice));
+        CE_TRY(hipMemcpy(e->row_agent, order.data(), P * sizeof(int32_t), hipMemcpyHostToDevice));
     }
     const size_t sizes[5] = {E * P * 3 * H * sizeof(float), E * P * sizeof(float),
                              E * CE_MULTI_INFO * sizeof(float), E * sizeof(int32_t),
@@ -318,6 +327,8 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     a.reset_perm = e->reset_perm;
     a.epoch_perm = e->epoch_perm;
     a.agent_row = e->agent_row;
+    a.row_agent = e->row_agent;
+    if (const char *ag = std::getenv("CE_NN_AGENT")) e->agent_order = std::strcmp(ag, "agent") == 0;
     *out = e;
     return CE_OK;
 }
@@ -329,7 +340,7 @@ void ce_nn_destroy(ce_nn_engine *e) {
     void *dev[] = {e->X, e->label, e->theta_buf[0], e->theta_buf[1], e->g_buf[0], e->g_buf[1],
                    e->theta0, e->gU, e->loss_b, e->part_u, e->part_c, e->rw, e->rg,
                    e->al, e->sw, e->sg, e->hl, e->hsg, e->step, e->cursor,
-                   e->order, e->order_sel, e->reset_perm, e->epoch_perm, e->agent_row,
+                   e->order, e->order_sel, e->reset_perm, e->epoch_perm, e->agent_row, e->row_agent,
                    e->d_act, e->d_out, e->diag};
     for (void *p : dev)
         if (p) (void)hipFree(p);

@@ -109,6 +109,7 @@ struct NnArgs {
     const int32_t *reset_perm;     // [E][N] the shuffle every reset draws
     const int32_t *epoch_perm;     // [E][N] the shuffle every epoch end draws
     const int32_t *agent_row;      // [P] OptVecEnv row of agent p (sorted names)
+    const int32_t *row_agent;      // [P] agent of OptVecEnv row r (the inverse)
     const float *act;              // [E][P] rows
     float *obs;                    // [E][P][3H] rows
     float *reward;                 // [E][P] rows
@@ -804,6 +805,115 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_kernel(NnArgs a) {
             }
         }
         __syncthreads();
+    }
+    nn_block_sum<5, kNnChunk>(v, red);
+    if (tid == 0) {
+        double *o = a.part_c + (e * a.nchunk + chunk) * 5;
+        for (int k = 0; k < 5; ++k) o[k] = v[k];
+    }
+}
+
+// The same step in OBSERVATION-ROW order (the default; nn_agent_kernel walks
+// agents, CE_NN_AGENT=agent): block = kNnChunk consecutive obs rows of one
+// env, thread = row r, agent p = row_agent[r].
+//   - The block's observation rows are one contiguous run of kNnChunk * 3H
+//     floats: staged in LDS at the run's 16-byte phase, then written as
+//     float4s (plus at most 3 head and 3 tail floats) instead of 4-byte
+//     stores around the holes the other agents' rows leave in agent order.
+//   - The adjusted rings are kept in row order, so their reads and writes
+//     stay contiguous; theta, theta' and the gradients are gathered through
+//     row_agent, which in sorted-name order is runs of consecutive agents.
+//   - The per-block sums (|theta'|, |w~|, |g~|, g, |dg|) are sums over the
+//     same agents in another order.
+__global__ __launch_bounds__(kNnChunk) void nn_agent_rows_kernel(NnArgs a) {
+#pragma clang fp contract(off)
+    extern __shared__ float stage[];               // [kNnChunk * 3H + 4] rows at the run's phase
+    __shared__ float lobs[kNnMaxH];
+    __shared__ double red[(kNnChunk / 64) * 5];
+    const size_t e = blockIdx.y, ps = a.Ps, E = a.E;
+    const int chunk = blockIdx.x, tid = threadIdx.x, H = a.H, W = 3 * H;
+    const int r0 = chunk * kNnChunk;
+    const int r = r0 + tid;
+    const bool on = r < a.P;
+    const int rc = on ? r : r0;
+    const NnStepScalars sc = nn_step_scalars(a, e);
+    const int s = sc.s, slot = sc.slot;
+    const size_t plane = E * ps;
+    const size_t eb = e * ps;
+
+    // ---- every load up front: the agent, its four values, its ring ages
+    const int p = a.row_agent[rc];
+    const float to = a.theta[eb + p], tn = a.theta_n[eb + p];
+    const float gp = a.gprev[eb + p], g = a.gN[eb + p];
+    float rwv[kNnMaxH], rgv[kNnMaxH];
+#pragma unroll
+    for (int k = 1; k < kNnMaxH; ++k) {
+        if (k < H && k < s) {                       // block-uniform
+            const size_t sl = ((slot - k) % H + H) % H;
+            rwv[k] = a.rw[sl * plane + eb + rc];
+            rgv[k] = a.rg[sl * plane + eb + rc];
+        } else {
+            rwv[k] = rgv[k] = -1.0f;                // clip(0) - 1: the reset zeros
+        }
+    }
+    if (tid < H) {
+        const int k = tid;
+        double lk = 0.0;
+        if (k == 0) lk = sc.adj_l;
+        else if (k < s) lk = a.al[(((slot - k) % H + H) % H) * E + e];
+        lobs[k] = static_cast<float>(clip100(lk) - 1.0);
+    }
+    const double adj_w = nn_ratio(tn, to);
+    const double adj_g = nn_ratio(g, gp);
+    const float ow = static_cast<float>(clip100(adj_w) - 1.0);
+    const float og = static_cast<float>(clip100(adj_g) - 1.0);
+    double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    if (on) {
+        v[0] = fabs(static_cast<double>(tn));
+        v[1] = fabs(adj_w);
+        v[2] = fabs(adj_g);
+        v[3] = g;
+        v[4] = fabs(static_cast<double>(g) - static_cast<double>(gp));
+        a.rw[slot * plane + eb + r] = ow;
+        a.rg[slot * plane + eb + r] = og;
+        if (sc.wipe) a.theta_n[eb + p] = a.theta0[eb + p];
+    }
+    // ---- the block's rows: global floats [g0, g0 + n), staged at LDS
+    // position (global index - g0) + (g0 & 3), so 16-byte global chunks are
+    // 16-byte LDS chunks
+    const size_t g0 = (e * static_cast<size_t>(a.P) + r0) * W;
+    const int off = static_cast<int>(g0 & 3);
+    __syncthreads();                                // lobs ready
+    if (on) {
+        float *st = stage + off + tid * W;
+#pragma unroll
+        for (int k = 0; k < kNnMaxH; ++k) {
+            if (k < H) {
+                st[k] = sc.wipe ? -1.0f : (k == 0 ? ow : rwv[k]);
+                st[H + k] = sc.wipe ? -1.0f : lobs[k];
+                st[2 * H + k] = sc.wipe ? -1.0f : (k == 0 ? og : rgv[k]);
+            }
+        }
+    }
+    __syncthreads();
+    const int n = (a.P - r0 < kNnChunk ? a.P - r0 : kNnChunk) * W;
+    const size_t a0 = (g0 + 3) & ~size_t(3), a1 = (g0 + n) & ~size_t(3);
+    float *obs = a.obs;
+#ifdef CE_NN_DIAG_NOOBS
+    if (n < 0)   // timing diagnostic: no observation stores
+#endif
+    {
+        if (a1 > a0) {
+            const int head = static_cast<int>(a0 - g0), tail = static_cast<int>(g0 + n - a1);
+            if (tid < head) obs[g0 + tid] = stage[off + tid];
+            if (tid < tail) obs[a1 + tid] = stage[off + static_cast<int>(a1 - g0) + tid];
+            const int nb = static_cast<int>((a1 - a0) >> 2);
+            const float4 *src = reinterpret_cast<const float4 *>(stage + off + head);
+            float4 *dst = reinterpret_cast<float4 *>(obs + a0);
+            for (int i = tid; i < nb; i += kNnChunk) dst[i] = src[i];
+        } else {
+            for (int i = tid; i < n; i += kNnChunk) obs[g0 + i] = stage[off + i];
+        }
     }
     nn_block_sum<5, kNnChunk>(v, red);
     if (tid == 0) {
