@@ -13,7 +13,12 @@ entry turns float32 summation-order noise into an arbitrary ratio:
 * formula parity on the engine's own state: every observation entry, the
   loss ratio, and the info statistics recomputed in numpy from the engine's
   theta / gradient / loss sequence with the reference's formulas
-  (multioptlrs.py:90-127), to float32 rounding of the float64 result.
+  (multioptlrs.py:90-127), to float32 rounding of the float64 result;
+* observation parity with the live oracle's own rows, for the newest w~,
+  l~ and g~ entries: the state tolerance carried through each entry's ratio
+  (clipping to +-100 only shrinks a difference), on the entries whose
+  denominator is at least 1e-3 of the vector's max (at least a quarter of
+  them must qualify).
 """
 import numpy as np
 import pytest
@@ -67,6 +72,28 @@ def _run_engine(ds, hidden, seeds, acts, max_batches, H=5):
     return P, rows, rec
 
 
+def _oracle_rows(obs_o, names):
+    if isinstance(obs_o, dict):
+        return np.stack([np.asarray(obs_o[n], np.float64) for n in names])
+    return np.asarray(obs_o, np.float64)
+
+
+def _ratio_close(got, want, num, den, what, state_tol=1e-4):
+    """Observation entries clip(num / |den|) - 1 (float32) from the engine
+    vs the oracle's own.  The engine's num and den are within state_tol of
+    the vectors' max of the oracle's (the state checks), so an entry's ratio
+    is within state_tol (max|num| + |ratio| max|den|) / |den|; twice that,
+    on the entries with |den| >= 1e-3 max|den| (a quarter at least)."""
+    num = np.abs(np.asarray(num, np.float64))
+    den = np.abs(np.asarray(den, np.float64))
+    mask = den >= 1e-3 * den.max()
+    assert mask.mean() >= 0.25, (what, mask.mean())
+    w = want[mask]
+    tol = 2 * state_tol * (num.max() + np.abs(w + 1) * den.max()) / den[mask] + 1e-6
+    err = np.abs(got[mask].astype(np.float64) - w)
+    assert np.all(err <= tol), (what, float((err - tol).max()))
+
+
 def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state_tol=1e-4):
     """acts_env: [T][P] actions in row order for env i."""
     P = rows.size
@@ -84,6 +111,8 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
     g_prev = None           # engine gradient of the previous step (None after a reset)
     l_prev = None
     ring = []               # engine's age-0 obs entries of earlier steps this episode
+    th_o_prev = th0.astype(np.float64)   # the oracle's theta and gradient before the step
+    g_o_prev = None
     for t in range(acts_env.shape[0]):
         step = rec['steps'][t]
         act_rows = acts_env[t]
@@ -117,7 +146,15 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
             env.reset()
             assert np.array_equal(st['order'][i], env.order()), t
             theta_prev, g_prev, l_prev, ring = th0.astype(np.float64), None, None, []
+            th_o_prev, g_o_prev = th0.astype(np.float64), None
             continue
+        # ---- observation parity with the oracle's rows (well-conditioned entries)
+        rows_o = _oracle_rows(obs_o, names)
+        _ratio_close(obs[:, 0], rows_o[:, 0], th_o, th_o_prev, ('w', t))
+        if g_o_prev is not None:
+            _ratio_close(obs[:, 2 * H], rows_o[:, 2 * H], g_o, g_o_prev, ('g', t))
+        assert float(obs[0, H]) == pytest.approx(float(rows_o[0, H]), rel=1e-3, abs=1e-3)
+        th_o_prev, g_o_prev = np.asarray(th_o, np.float64).copy(), np.asarray(g_o, np.float64).copy()
         w_new = _obs_form(_ratio(theta_after, theta_prev))
         assert np.array_equal(obs[:, 0], w_new), t
         if g_prev is not None:
