@@ -157,7 +157,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     __shared__ double red_s[kLrWaves][4][kWave];        // per-wave gradient partials
     __shared__ double red_l[kLrWaves][kLrEnvs];         // per-wave -log CE partials
     __shared__ double red_h[kLrWaves][kLrEnvs];         // per-wave hit counts
-    __shared__ double wsh[kLrEnvs][P_MAX];              // W' of the group's envs
+    __shared__ __attribute__((aligned(16))) double wsh[kLrEnvs][P_MAX];   // W' of the group's envs
 #ifdef CE_DIAG
     unsigned long long stamps[kStamps] = {0};
     stamps[6] = __builtin_amdgcn_s_memrealtime();
@@ -242,6 +242,9 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
 
     // ---- W' = W - a (optimize.py:74-75); forward B operand: the margin
     // w'_f0 - w'_f1 of feature 4k + h for env c
+    // (every wave loads the W / action pairs it needs itself: forming W'
+    // once per workgroup in LDS behind a barrier measured slower at 4, 8
+    // and 16 waves, 6.16 / 6.33 / 6.97 against 5.98 / 6.04 / 6.99 us)
     double wd[NKF];
 #pragma unroll
     for (int k = 0; k < NKF; ++k) {
