@@ -664,7 +664,12 @@ def main():
         modes['serial'] = _timed(torch, dist, run_ser, args.steps)
         run_graph(args.warmup)
         modes['no_gather'] = _timed(torch, dist, run_graph, args.steps)
-        elapsed = modes['pipelined']
+        # both schedules run every step AND its all-gather inside the timed
+        # region; `value` is the faster of the two (at world 1 the pipelined
+        # one's cross-stream waits cost more than the copy it hides: 14.2 vs
+        # 7.7 us per step, profiles/r02_bench_force_gather.json)
+        gather_mode = min(('pipelined', 'serial'), key=lambda m: modes[m])
+        elapsed = modes[gather_mode]
     else:
         primary = run_graph
         primary(args.warmup)
@@ -730,6 +735,7 @@ def main():
             line['value_no_gather'] = units / modes['no_gather']
             line['ms_per_step_modes'] = {k: v / args.steps * 1e3 for k, v in modes.items()}
             line['gather_bytes_per_rank'] = shard.layout.nbytes
+            line['gather_mode'] = gather_mode
             line['gather_graph'] = gather_graph
         line['cpu_baseline'] = cpu
         if host_rate is not None:
