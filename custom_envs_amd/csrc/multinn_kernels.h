@@ -827,7 +827,8 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_kernel(NnArgs a) {
 //     same agents in another order.
 __global__ __launch_bounds__(kNnChunk) void nn_agent_rows_kernel(NnArgs a) {
 #pragma clang fp contract(off)
-    extern __shared__ float stage[];               // [kNnChunk * 3H + 4] rows at the run's phase
+    extern __shared__ float4 stage4[];             // [kNnChunk * 3H + 4] rows at the run's phase
+    float *stage = reinterpret_cast<float *>(stage4);
     __shared__ float lobs[kNnMaxH];
     __shared__ double red[(kNnChunk / 64) * 5];
     const size_t e = blockIdx.y, ps = a.Ps, E = a.E;
@@ -879,10 +880,11 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_rows_kernel(NnArgs a) {
         if (sc.wipe) a.theta_n[eb + p] = a.theta0[eb + p];
     }
     // ---- the block's rows: global floats [g0, g0 + n), staged at LDS
-    // position (global index - g0) + (g0 & 3), so 16-byte global chunks are
-    // 16-byte LDS chunks
+    // position (global index - g0) + off, off = the run's float phase within
+    // a 16-byte unit of the ACTUAL address (a caller's obs pointer need only
+    // be 4-byte aligned), so 16-byte global chunks are 16-byte LDS chunks
     const size_t g0 = (e * static_cast<size_t>(a.P) + r0) * W;
-    const int off = static_cast<int>(g0 & 3);
+    const int off = static_cast<int>((reinterpret_cast<uintptr_t>(a.obs + g0) >> 2) & 3);
     __syncthreads();                                // lobs ready
     if (on) {
         float *st = stage + off + tid * W;
@@ -897,7 +899,8 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_rows_kernel(NnArgs a) {
     }
     __syncthreads();
     const int n = (a.P - r0 < kNnChunk ? a.P - r0 : kNnChunk) * W;
-    const size_t a0 = (g0 + 3) & ~size_t(3), a1 = (g0 + n) & ~size_t(3);
+    const size_t a0 = g0 + ((4 - off) & 3);             // first 16-byte-aligned float
+    const size_t a1 = a0 + ((g0 + n - a0) & ~size_t(3)) * (g0 + n >= a0);   // end of whole units
     float *obs = a.obs;
 #ifdef CE_NN_DIAG_NOOBS
     if (n < 0)   // timing diagnostic: no observation stores
