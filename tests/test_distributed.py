@@ -123,8 +123,11 @@ def test_packed_layout_segments_are_aligned_and_disjoint():
     assert glob['obs'].shape == (28, 15)
 
 
-def test_gloo_world2_gather_equals_single_rank(lr_dataset):
+@pytest.mark.parametrize('world', [2, 3])
+def test_gloo_world2_gather_equals_single_rank(lr_dataset, world):
+    """5 envs over 2 ranks (3 + 2) and 3 ranks (2 + 2 + 1)."""
     import torch.multiprocessing as mp
     features, targets = lr_dataset
     expected = _rollout(features, targets, 5, 0, 1)
-    mp.spawn(_worker, args=(2, _free_port(), features, targets, expected), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), features, targets, expected), nprocs=world,
+             join=True)
