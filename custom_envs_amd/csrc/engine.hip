@@ -128,6 +128,7 @@ struct ce_engine {
     // per step direct vs 8.0 graph; 100 and 2000 steps equal.
     int many_direct = 32;
     int lr_waves = 0;         // CE_LR_WAVES: force the two-class MFMA kernel's wave count
+    int gen_tail = 1;         // CE_GEN_TAIL=0: the runtime-shape kernel's last feature on MFMA too
     unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
 };
 
@@ -175,6 +176,7 @@ ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs
     const int P = e->cfg.n_features * e->cfg.n_classes;
     a.p_mul = (65536 + P - 1) / P;
     a.lr_waves = e->lr_waves;
+    a.gen_tail = e->gen_tail;
     return a;
 }
 
@@ -438,6 +440,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     e->mlp = mlp;
     if (const char *md = std::getenv("CE_MANY_DIRECT")) e->many_direct = std::atoi(md);
     if (const char *lw = std::getenv("CE_LR_WAVES")) e->lr_waves = std::atoi(lw);
+    if (const char *gt = std::getenv("CE_GEN_TAIL")) e->gen_tail = std::atoi(gt);
     // experiment switch: launch one phase only, to time each kernel alone
     if (const char *ph = std::getenv("CE_MLP_PHASES")) {
         if (std::strcmp(ph, "train") == 0) e->mlp_phases = 1;

@@ -19,7 +19,15 @@ using GenFn = void (*)(const StepArgs<double> &, hipStream_t);
 template <int NK>
 void launch_nk(const StepArgs<double> &a, hipStream_t stream) {
     const int grid = (a.E + kGenWaves - 1) / kGenWaves;
-    hipLaunchKernelGGL((optimize_mfma_kernel<NK>), dim3(grid), dim3(kGenBlock),
+    // F = 16 (FT - 1) + 1 with the full data set: the last feature on the VALU
+    if constexpr (NK % 4 == 1 && NK > 1) {
+        if (a.F == 4 * (NK - 1) + 1 && a.B == a.N && a.gen_tail) {
+            hipLaunchKernelGGL((optimize_mfma_kernel<NK, true>), dim3(grid), dim3(kGenBlock),
+                               gen_lds_bytes((NK + 3) / 4), stream, a);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((optimize_mfma_kernel<NK, false>), dim3(grid), dim3(kGenBlock),
                        gen_lds_bytes((NK + 3) / 4), stream, a);
 }
 
@@ -27,9 +35,10 @@ template <int... NKs>
 struct Table {
     static constexpr GenFn steps[sizeof...(NKs)] = {launch_nk<NKs>...};
     static int set_lds_limits() {
-        const void *fns[] = {reinterpret_cast<const void *>(optimize_mfma_kernel<NKs>)...};
-        const int ft[] = {((NKs + 3) / 4)...};
-        for (size_t i = 0; i < sizeof...(NKs); ++i)
+        const void *fns[] = {reinterpret_cast<const void *>(optimize_mfma_kernel<NKs, false>)...,
+                             reinterpret_cast<const void *>(optimize_mfma_kernel<NKs, (NKs % 4 == 1 && NKs > 1)>)...};
+        const int ft[] = {((NKs + 3) / 4)..., ((NKs + 3) / 4)...};
+        for (size_t i = 0; i < 2 * sizeof...(NKs); ++i)
             CE_HIP(hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize,
                                        static_cast<int>(gen_lds_bytes(ft[i]))));
         return CE_OK;

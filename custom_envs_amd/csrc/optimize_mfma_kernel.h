@@ -228,9 +228,15 @@ __device__ __forceinline__ gen_d4 gen_forward(const double (&wb)[NK], const doub
 // NK = ceil(F / 4) forward k-steps (a compile-time count, so the MFMA
 // chains are straight-line code with their LDS reads issued together),
 // FT = ceil(F / 16) gradient feature tiles.
-template <int NK>
+// TAIL (F = 16 (FT - 1) + 1: F = 17, 33, 49 -- the 7x7 image sets): in the
+// full-data LDS stream the last feature is done on the VALU instead of by a
+// whole padded MFMA k-step (forward: 4 FMAs per lane per sub-block in place
+// of 1 MFMA) and a whole padded 16-feature gradient tile (4 FMAs in place of
+// 4 MFMAs), 29 -> 24 f64 MFMAs per 16 rows at F = 49.
+template <int NK, bool TAIL>
 __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<double> a) {
     constexpr int FT = (NK + 3) / 4;
+    static_assert(!TAIL || (NK % 4 == 1 && NK > 1), "TAIL: the last k-step and the last tile hold one feature");
     constexpr int RS = gen_stride(FT);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & (kWave - 1);
@@ -255,6 +261,21 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
         const int idx = own ? f * K + c : 0;
         const double w = a.W[pbase + idx] - static_cast<double>(a.act[pbase + idx]);
         wb[k] = own ? w : 0.0;
+    }
+
+    // TAIL: W'[fl][class h + 4q] of the last feature fl = F - 1 (forward C
+    // layout), and the lane's running sum of x[row][fl] D[row][class c]
+    constexpr int FL = 4 * (NK - 1);
+    double wt[4] = {0.0, 0.0, 0.0, 0.0};
+    double gtail = 0.0;
+    if constexpr (TAIL) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = h + 4 * q;
+            const int idx = k < K ? FL * K + k : 0;
+            const double w = a.W[pbase + idx] - static_cast<double>(a.act[pbase + idx]);
+            wt[q] = k < K ? w : 0.0;
+        }
     }
 
     gen_d4 g[FT];
@@ -324,6 +345,19 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
             // so the matrix pipe runs while this wave does its VALU work
             auto forward = [&](int sb) {
                 const double *xs = xb + sb * 16 * RS;
+                if constexpr (TAIL) {
+                    double av[NK - 1], wv[NK - 1];
+#pragma unroll
+                    for (int k = 0; k < NK - 1; ++k) {
+                        av[k] = xs[c * RS + 4 * k + h];
+                        wv[k] = wb[k];
+                    }
+                    gen_d4 z = gen_forward<NK - 1>(wv, av);
+                    const double xl = xs[c * RS + FL];          // row c, the last feature
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) z[q] = fma(wt[q], xl, z[q]);
+                    return z;
+                }
                 double av[NK];
 #pragma unroll
                 for (int k = 0; k < NK; ++k) av[k] = xs[c * RS + 4 * k + h];
@@ -341,12 +375,15 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
                     double bd[4];
                     gen_softmax(z, h, K, y, d, prod, hits);
                     gen_grad(d, dsh, c, h, bd);
+                    constexpr int FTM = TAIL ? FT - 1 : FT;     // tiles on the matrix pipe
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
+                    for (int r = 0; r < 4; ++r) {
 #pragma unroll
-                        for (int t = 0; t < FT; ++t)
+                        for (int t = 0; t < FTM; ++t)
                             g[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(
                                 xs[(4 * r + h) * RS + 16 * t + c], bd[r], g[t], 0, 0, 0);
+                        if constexpr (TAIL) gtail = fma(xs[(4 * r + h) * RS + FL], bd[r], gtail);
+                    }
                 } else {
                     gen_softmax(z, h, K, y, d, fprod, fhits);
                 }
@@ -369,6 +406,15 @@ __global__ __launch_bounds__(kGenBlock) void optimize_mfma_kernel(StepArgs<doubl
         floss -= log_pos(fprod);
         objective = wave_sum(floss) / N;
         accuracy = wave_sum(static_cast<double>(fhits)) / N;
+    }
+
+    // TAIL: G[fl][class c] = the lane sums over the 4 row groups h; it is
+    // register 0 of the last tile on the h = 0 lanes (full data only; a
+    // minibatch ran the last tile on the matrix pipe)
+    if constexpr (TAIL) {
+        gtail = fold_pair<16>(gtail, gtail);
+        gtail = fold_pair<32>(gtail, gtail);
+        if (full) g[FT - 1][0] = gtail;
     }
 
     // ---- recurrences (optimize.py:78-92) and outputs

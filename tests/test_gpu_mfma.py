@@ -24,10 +24,11 @@ def _need_gpu():
         pytest.fail('GPU tests need a ROCm device (run under gpurun)')
 
 
-def _engine(dataset, num_envs, batch_size=None, generic=False, lr=False, lr_waves=0, **kw):
+def _engine(dataset, num_envs, batch_size=None, generic=False, lr=False, lr_waves=0, gen_tail=1,
+            **kw):
     from custom_envs_amd.engine import OptimizeEngine
     flags = {'CE_GENERIC': '1' if generic else '0', 'CE_LR_MFMA': '1' if lr else '0',
-             'CE_LR_WAVES': str(lr_waves)}
+             'CE_LR_WAVES': str(lr_waves), 'CE_GEN_TAIL': str(gen_tail)}
     old = {k: os.environ.get(k) for k in flags}
     os.environ.update(flags)
     try:
@@ -115,11 +116,15 @@ def test_image_shape_many_envs(batch_size):
     eng.close()
 
 
+@pytest.mark.parametrize('gen_tail', [1, 0])
 @pytest.mark.parametrize('shape', [(4, 3), (17, 2), (33, 7), (64, 16), (49, 10), (1, 5)])
-def test_every_feature_tile_count(shape):
+def test_every_feature_tile_count(shape, gen_tail):
+    """Every feature-tile count; F = 17, 33, 49 (one feature in the last
+    k-step and tile) with the last feature on the VALU (gen_tail=1, the
+    default for the full data set) and on the matrix pipe (gen_tail=0)."""
     F, K = shape
     ds = _classes(300, F, K, F + K)
-    eng = _engine(ds, 9, None, generic=True)
+    eng = _engine(ds, 9, None, generic=True, gen_tail=gen_tail)
     assert eng.step_kernel == 'optimize_mfma_kernel<%d>' % ((F + 3) // 4)
     _check(ds, None, eng, [0, 8], 41)
     eng.close()
