@@ -212,6 +212,10 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     // the wave waits for memory once instead of once per dependent round trip
     const int step_prev = a.step[ec];
     const float act = a.act[ec * P + r];
+    // the reset point: loaded here, not after the stores -- vmcnt counts
+    // stores too, so a load issued after them would make its first use wait
+    // for every one of them to complete
+    const float th_init = i < P ? a.init[i] : 0.0f;
     const float th0 = a.theta[ec * P + ic];
     const float g0 = a.grad[ec * P + ic];
     float hl_v[kRawHist], hg_v[kRawHist], hw_v[kRawHist];
@@ -358,7 +362,6 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
         a.done[e * P + r] = terminal ? 1 : 0;
     }
 
-    const float th_init = i < P ? a.init[i] : 0.0f;
     float g_init, l_init;
     rosenbrock_lane<P>(th_init, i, g_init, l_init);     // all lanes: it shuffles
     if (wipe && on) {
