@@ -81,17 +81,20 @@ void launch_lr_w(const StepArgs<double> &a, hipStream_t stream) {
 }
 
 // Wave count: 4 waves per workgroup (one per SIMD, tiles 4 at a time,
-// software-pipelined) when the grid fills the chip and every wave gets
-// whole groups of 4 tiles: 5.95 us per 4096-env launch at 256 x 10, against
-// 6.06 at 8 waves and 7.0 at 16 (one tile per wave, 4 waves per SIMD: its
-// row phase is 2.5x cheaper per tile, but its waves start up to 3.3 us
-// apart).  Otherwise 8 waves, which halve each wave's rows
-// for small grids.  a.lr_waves = 4, 8 or 16 (CE_LR_WAVES at ce_create)
+// software-pipelined) when every wave gets whole groups of 4 tiles and
+// either the grid fills the chip or there is one group per wave: at
+// 256 x 10, 5.96 us per 4096-env launch against 6.06 at 8 waves and 7.0 at
+// 16, and 5.44 / 5.54 / 6.49 at 1024 envs (the row work is
+// the same f64 work at every wave count; more waves cost more in the fixed
+// phases).  Otherwise 8 waves, which halve each wave's rows when a small
+// grid has many of them.  a.lr_waves = 4, 8 or 16 (CE_LR_WAVES at ce_create)
 // forces one.
 template <int NKF>
 void launch_lr(const StepArgs<double> &a, hipStream_t stream) {
     const int groups = (a.E + kLrEnvs - 1) / kLrEnvs;
-    const int w = a.lr_waves ? a.lr_waves : groups >= 256 && lr_mode(a.N, 4) == 3 ? 4 : 8;
+    const int ntiles = (a.N + 15) / 16;
+    const int w = a.lr_waves ? a.lr_waves
+                             : lr_mode(a.N, 4) == 3 && (groups >= 256 || ntiles <= 16) ? 4 : 8;
     if (w == 16) launch_lr_w<NKF, 16>(a, stream);
     else if (w == 4) launch_lr_w<NKF, 4>(a, stream);
     else launch_lr_w<NKF, 8>(a, stream);
