@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-2 evidence in one call: GPU tests, smoke, the default bench (with the
+# Round evidence in one call (OUT names the result directory): GPU tests, smoke, the default bench (with the
 # CPU baseline) and the driver's 20-step form, rocprofv3 kernel trace + PMC
 # passes of the benchmark kernel, and the config-3 / config-5 / NN / image-
 # shape workloads with their kernel traces.  Every GPU step has its own time
 # limit; any failure stops the script.
 set -u
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/r2final
+OUT=${OUT:-gpurun_out/evidence}
 mkdir -p $OUT/pmc
 export TMPDIR=/tmp
 fatal() { case $1 in 0) ;; *) echo "GPU step failed (rc=$1), stopping"; exit $1;; esac; }
