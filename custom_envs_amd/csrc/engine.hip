@@ -92,8 +92,6 @@ struct ce_engine {
     int P = 0, obs_dim = 0;
     bool mlp = false;  // CE_PROBLEM_MLP
     bool mlp_split = false;  // two launches per step (CE_MLP_SPLIT=1 or CE_MLP_PHASES)
-    int n_cus = 1;           // compute units of the device (persistent MLP grid)
-    bool mlp_persist = false;  // CE_MLP_PERSIST=1: the 8-wave persistent step kernel
     int mlp_phases = 3;  // bit 0: train kernel, bit 1: info kernel (CE_MLP_PHASES, profiling)
     size_t tsize = 8;  // element size of W / W0
     size_t gsize = 8;  // element size of G (grad_hist)
@@ -129,6 +127,7 @@ struct ce_engine {
     int many_direct = 32;
     int lr_waves = 0;         // CE_LR_WAVES: force the two-class MFMA kernel's wave count
     int gen_tail = 1;         // CE_GEN_TAIL=0: the runtime-shape kernel's last feature on MFMA too
+    int lr_mode_cap = 3;      // CE_LR_MODE: cap on the two-class MFMA kernel's row-loop mode
     unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
 };
 
@@ -177,6 +176,7 @@ ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs
     a.p_mul = (65536 + P - 1) / P;
     a.lr_waves = e->lr_waves;
     a.gen_tail = e->gen_tail;
+    a.lr_mode_cap = e->lr_mode_cap;
     return a;
 }
 
@@ -223,15 +223,6 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
         const bool even = (e->P & 1) == 0;   // pair accesses aligned in every env
         if (reset) {
             hipLaunchKernelGGL(ce::mlp_reset_kernel, grid, block, 0, stream, a);
-        } else if (e->mlp_persist) {
-            // persistent: one 8-wave workgroup per CU (mlp_kernels.h)
-            const dim3 pgrid(std::min(e->cfg.num_envs, e->n_cus)), pblock(ce::kMlpStepBlock);
-            if (even)
-                hipLaunchKernelGGL(ce::mlp_persist_kernel<true>, pgrid, pblock, ce::kMlpStepRingLds,
-                                   stream, a);
-            else
-                hipLaunchKernelGGL(ce::mlp_persist_kernel<false>, pgrid, pblock, ce::kMlpStepRingLds,
-                                   stream, a);
         } else if (!e->mlp_split) {
             if (even) hipLaunchKernelGGL(ce::mlp_step_kernel<true>, grid, block, 0, stream, a);
             else hipLaunchKernelGGL(ce::mlp_step_kernel<false>, grid, block, 0, stream, a);
@@ -441,6 +432,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     if (const char *md = std::getenv("CE_MANY_DIRECT")) e->many_direct = std::atoi(md);
     if (const char *lw = std::getenv("CE_LR_WAVES")) e->lr_waves = std::atoi(lw);
     if (const char *gt = std::getenv("CE_GEN_TAIL")) e->gen_tail = std::atoi(gt);
+    if (const char *lm = std::getenv("CE_LR_MODE")) e->lr_mode_cap = std::atoi(lm);
     // experiment switch: launch one phase only, to time each kernel alone
     if (const char *ph = std::getenv("CE_MLP_PHASES")) {
         if (std::strcmp(ph, "train") == 0) e->mlp_phases = 1;
@@ -448,7 +440,6 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         e->mlp_split = true;
     }
     if (const char *sp = std::getenv("CE_MLP_SPLIT")) e->mlp_split = e->mlp_split || sp[0] == '1';
-    if (const char *pp = std::getenv("CE_MLP_PERSIST")) e->mlp_persist = !e->mlp_split && pp[0] == '1';
     if (mlp) {
         const int F = cfg->n_features, H = cfg->n_hidden, K = cfg->n_classes;
         e->P = F * H + H + H * K + K;
@@ -478,12 +469,6 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
 
     const size_t E = cfg->num_envs, N = cfg->n_rows, F = cfg->n_features, P = e->P;
     if (mlp) {
-        CE_TRY(hipDeviceGetAttribute(&e->n_cus, hipDeviceAttributeMultiprocessorCount, cfg->device));
-        const int lds = static_cast<int>(ce::kMlpStepRingLds);
-        CE_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(ce::mlp_persist_kernel<true>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        CE_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(ce::mlp_persist_kernel<false>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         CE_TRY(hipMalloc(&e->X, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->Xs, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
@@ -558,8 +543,8 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         if (hipMemcpy(e->X, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice) !=
             hipSuccess)
             return bail(fail(CE_EHIP, "ce_create: dataset upload failed"));
-        e->kernel_name = "optimize_lr_mfma_kernel<" +
-                         std::to_string((cfg->n_features + 3) / 4) + ">";
+        e->kernel_name = ce::lr_kernel_name(cfg->num_envs, cfg->n_rows, cfg->n_features,
+                                            e->lr_waves, e->lr_mode_cap);
     } else if (e->gen_ft) {
         // [Npad][RS] float64: F features, zeros to 16 FT + 1, the label as a
         // double in the last column; rows N..Npad-1 are zeros with label -1
@@ -775,7 +760,7 @@ const char *ce_step_kernel(const ce_engine *e) {
     if (!e) return "";
     if (e->mlp)
         return e->mlp_split ? "mlp_train_kernel+mlp_info_kernel"
-                            : e->mlp_persist ? "mlp_persist_kernel" : "mlp_step_kernel";
+                            : "mlp_step_kernel";
     return e->kernel_name.c_str();
 }
 

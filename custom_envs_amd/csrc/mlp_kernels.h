@@ -185,27 +185,6 @@ __device__ __forceinline__ unsigned lds_addr(const void *p) {
         (const __attribute__((address_space(3))) char *)(p)));
 }
 
-// One info chunk's operands from an LDS-DMA slot: T X float4s at xa + 1024 q
-// and 4 W1 pairs at wa + 256 jj, then a wait for all of them.
-template <int T>
-__device__ __forceinline__ void lds_read_slot(unsigned xa, unsigned wa, nt_f4 (&x)[T], nt_f2 (&w)[4]) {
-    static_assert(T == 4, "offsets below are written out for T = 4");
-    asm volatile("ds_read_b128 %0, %4\n\t"
-                 "ds_read_b128 %1, %4 offset:1024\n\t"
-                 "ds_read_b128 %2, %4 offset:2048\n\t"
-                 "ds_read_b128 %3, %4 offset:3072"
-                 : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
-                 : "v"(xa));
-    asm volatile("ds_read_b64 %0, %4\n\t"
-                 "ds_read_b64 %1, %4 offset:256\n\t"
-                 "ds_read_b64 %2, %4 offset:512\n\t"
-                 "ds_read_b64 %3, %4 offset:768\n\t"
-                 "s_waitcnt lgkmcnt(0)"
-                 : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
-                 : "v"(wa)
-                 : "memory");
-}
-
 // block-wide p[0:n] = 0 with 16-B stores between a scalar head and tail
 __device__ __forceinline__ void zero_floats(float *p, int n, int tid, int nthreads) {
     int head = static_cast<int>(((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4);
@@ -271,28 +250,10 @@ __device__ __forceinline__ void write_grad(const MlpArgs &a, size_t e, int idx, 
     a.obs[e * (2 * static_cast<size_t>(a.P) + 1) + a.P + 1 + idx] = static_cast<float>(gn);
 }
 
-// Barriers of the phase bodies: the whole workgroup, or the 4 waves of one
-// half of an 8-wave workgroup (an LDS counter: each wave's lane 0 adds one
-// and waits for the count to reach its generation's end).
+// Barrier of the phase bodies: the whole workgroup.
 struct WgSync {
     __device__ __forceinline__ void operator()() const { __syncthreads(); }
 };
-struct GroupSync {
-    unsigned *ctr;
-    __device__ __forceinline__ void operator()() const {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if ((threadIdx.x & 63) == 0) {
-            const unsigned old =
-                __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const unsigned target = (old / 4 + 1) * 4;
-            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-                __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
-};
-
 // tid: thread index within the 256 threads that run the body; sync: their barrier
 template <bool A, typename Sync>
 __device__ __forceinline__ void mlp_train_body(const MlpArgs &a, const size_t e, MlpTrainShared &sh,
@@ -551,17 +512,9 @@ __global__ __launch_bounds__(kMlpBlock) void mlp_reset_kernel(MlpArgs a) {
 // updated weights, then the auto-reset of envs that just finished.  Each wave
 // takes T consecutive 32-sample tiles per pass: 2T accumulators live across
 // one sweep over K, so every W1 fragment a wave loads feeds 8T MFMAs.
-// R > 0: the chunk operands stream through a per-wave LDS-DMA ring of R
-// slots (ring: the half's kInfoRingBytes<T, R> of LDS) instead of registers.
-template <int T, int R>
-constexpr size_t info_slot_bytes() { return T * 1024 + 8 * 256; }
-template <int T, int R>
-constexpr size_t info_ring_bytes() { return 4 * R * info_slot_bytes<T, R>(); }
-
-template <int T, int D, int R, bool A, typename Sync>
+template <int T, int D, bool A, typename Sync>
 __device__ __forceinline__ void mlp_info_body(const MlpArgs &a, const size_t e, MlpInfoShared &sh,
-                                              MlpStamps &ms, const int tid, const Sync &sync,
-                                              char *ring = nullptr) {
+                                              MlpStamps &ms, const int tid, const Sync &sync) {
     unsigned long long *stamps = ms.stamps;
     (void)stamps;
     CE_STAMP(4);
@@ -598,54 +551,7 @@ __device__ __forceinline__ void mlp_info_body(const MlpArgs &a, const size_t e, 
         size_t toff[T];
 #pragma unroll
         for (int q = 0; q < T; ++q) toff[q] = (q < nt ? q : 0) * tstride;
-        if constexpr (R > 0) {
-            // LDS-DMA ring: slot = [T tiles][64 lanes][16 B] of X, then the
-            // chunk's 8 W1 rows [8][64 floats].  Each wave fills and reads only
-            // its own slots; a chunk is T + 8 DMA instructions, so R - 1
-            // chunks stay in flight behind s_waitcnt vmcnt((T + 8)(R - 1)).
-            // Refills past the last chunk repeat it into a slot nobody reads.
-            constexpr int kOps = T + 8;
-            constexpr size_t kSlot = info_slot_bytes<T, R>();
-            char *wring = ring + static_cast<size_t>(wave) * R * kSlot;
-            auto issue = [&](int c, int slot) {
-                char *dst = wring + slot * kSlot;
-#pragma unroll
-                for (int q = 0; q < T; ++q)
-                    __builtin_amdgcn_global_load_lds(
-                        (__attribute__((address_space(1))) void *)(xb + toff[q] + 256 * c),
-                        (__attribute__((address_space(3))) void *)(dst + q * 1024), 16, 0, 0);
-#pragma unroll
-                for (int r = 0; r < 8; ++r)
-                    __builtin_amdgcn_global_load_lds(
-                        (__attribute__((address_space(1))) void *)(W + (8 * c + r) * kMlpHidden + lane),
-                        (__attribute__((address_space(3))) void *)(dst + T * 1024 + r * 256), 4, 0, 0);
-            };
-#pragma unroll
-            for (int s = 0; s + 1 < R; ++s) issue(min(s, chunks - 1), s);
-            int slot = 0;
-            for (int c = 0; c < chunks; ++c) {
-                issue(min(c + R - 1, chunks - 1), slot == 0 ? R - 1 : slot - 1);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps * (R - 1)) : "memory");
-                // the slot is read with asm LDS loads: the compiler would
-                // otherwise guard every LDS read behind vmcnt(0), as it cannot
-                // tell which DMA fills which slot
-                const unsigned src = lds_addr(wring + slot * kSlot);
-                nt_f4 x[T];
-                nt_f2 w[4];
-                lds_read_slot<T>(src + lane * 16, src + T * 1024 + h * 1024 + li * 8, x, w);
-#pragma unroll
-                for (int q = 0; q < T; ++q) {
-                    const float xs[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        acc[q][0] = mfma32(w[jj].x, xs[jj], acc[q][0]);
-                        acc[q][1] = mfma32(w[jj].y, xs[jj], acc[q][1]);
-                    }
-                }
-                slot = slot + 1 == R ? 0 : slot + 1;
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the repeated tail refills
-        } else {
+        {
         // a D-deep pipeline of chunk operands: parts 0..T-1 are the
         // tiles' X float4s (refilled once the tile's 8 MFMAs issued), part T
         // the W1 pairs
@@ -789,70 +695,7 @@ __global__ __launch_bounds__(kMlpBlock, 2) void mlp_step_kernel(MlpArgs a) {
     const size_t e = blockIdx.x;
     mlp_train_body<A>(a, e, sh.t, ms, threadIdx.x, WgSync{});
     __syncthreads();
-    mlp_info_body<kStepInfoTiles, kStepInfoDepth, 0, A>(a, e, sh.i, ms, threadIdx.x, WgSync{});
-}
-
-// mlp_persist_kernel (CE_MLP_PERSIST=1): a persistent workgroup of 8 waves per
-// CU, measured slower (5.2 ms: the info half's 4 waves alone leave the matrix
-// pipe 40% idle even with an LDS-DMA operand ring).  Waves 0-3 run the train phase of the workgroup's env k while waves
-// 4-7 run the info phase of its env k - 1 (the info of an env needs its
-// train done; the two halves meet at one workgroup barrier per env), so the
-// train phase's HBM streaming runs under the info phase's MFMA work on the
-// same CU.  Each half synchronises internally on its own LDS counter barrier.
-// The workgroup holds more LDS than half a CU so exactly one lands per CU.
-// A = (P even): every env's parameter block starts at an even float and the
-// pair accesses are single 8-B / 16-B accesses; odd P runs the A = false
-// instance (one instance per launch keeps the code in the instruction cache).
-constexpr int kMlpStepBlock = 2 * kMlpBlock;
-#ifndef CE_MLP_RING
-#define CE_MLP_RING 4
-#endif
-constexpr int kStepInfoRing = CE_MLP_RING;   // LDS-DMA slots per info wave
-constexpr size_t kMlpStepRingLds = info_ring_bytes<kStepInfoTiles, kStepInfoRing>();
-static_assert(kMlpStepRingLds + sizeof(MlpTrainShared) + sizeof(MlpInfoShared) > 80 * 1024,
-              "the step workgroup must take more than half a CU's LDS");
-
-template <bool A>
-__global__ __launch_bounds__(kMlpStepBlock) void mlp_persist_kernel(MlpArgs a) {
-    __shared__ MlpTrainShared tsh;
-    __shared__ MlpInfoShared ish;
-    __shared__ unsigned ctr[2];
-    extern __shared__ char ring_lds[];   // kMlpStepRingLds (also: one workgroup per CU)
-    const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
-    const int tid = threadIdx.x & (kMlpBlock - 1);
-    if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
-    __syncthreads();
-    const GroupSync sync{&ctr[half]};
-    MlpStamps ms{};
-    // envs b, b + G, b + 2G, ... of this workgroup
-    const int G = gridDim.x, b = blockIdx.x;
-    const int n = (a.E - b + G - 1) / G;
-    // each half runs its own loop of n + 1 workgroup barriers (s_barrier
-    // counts waves, not program points)
-    if (half == 0) {
-        for (int k = 0; k <= n; ++k) {
-#ifdef CE_MLP_EXP_NO_TRAIN   // experiment builds: time the info half alone
-            if (false)
-#else
-            if (k < n)
-#endif
-                mlp_train_body<A>(a, static_cast<size_t>(b) + static_cast<size_t>(k) * G, tsh, ms, tid,
-                                  sync);
-            __syncthreads();
-        }
-    } else {
-        for (int k = 0; k <= n; ++k) {
-#ifdef CE_MLP_EXP_NO_INFO    // experiment builds: time the train half alone
-            if (false)
-#else
-            if (k > 0)
-#endif
-                mlp_info_body<kStepInfoTiles, kStepInfoDepth, kStepInfoRing, A>(
-                    a, static_cast<size_t>(b) + static_cast<size_t>(k - 1) * G, ish, ms, tid, sync,
-                    ring_lds);
-            __syncthreads();
-        }
-    }
+    mlp_info_body<kStepInfoTiles, kStepInfoDepth, A>(a, e, sh.i, ms, threadIdx.x, WgSync{});
 }
 
 // The split pair (CE_MLP_SPLIT=1, and CE_MLP_PHASES=train|info to time one
@@ -869,7 +712,7 @@ template <bool A>
 __global__ __launch_bounds__(kMlpBlock) void mlp_info_kernel(MlpArgs a) {
     __shared__ MlpInfoShared sh;
     MlpStamps ms{};
-    mlp_info_body<kSplitInfoTiles, kSplitInfoDepth, 0, A>(a, blockIdx.x, sh, ms, threadIdx.x,
+    mlp_info_body<kSplitInfoTiles, kSplitInfoDepth, A>(a, blockIdx.x, sh, ms, threadIdx.x,
                                                           WgSync{});
 }
 

@@ -35,7 +35,6 @@ struct ce_nn_engine {
     int32_t *step = nullptr, *cursor = nullptr, *order = nullptr, *order_sel = nullptr;
     int32_t *reset_perm = nullptr, *epoch_perm = nullptr, *agent_row = nullptr;
     int32_t *row_agent = nullptr;
-    bool agent_order = false;   // CE_NN_AGENT=agent: nn_agent_kernel (agent order) instead of rows
     float *d_act = nullptr, *h_act = nullptr;
     size_t off[5] = {0};
     size_t out_bytes = 0;
@@ -87,11 +86,7 @@ void launch_step(ce_nn_engine *e, const float *act, const ce_multi_outputs &o, h
     hipLaunchKernelGGL(ce::nn_grad_kernel, dim3(a.E), dim3(ce::kNnBlock), a.lds_bytes, s, a);
     hipLaunchKernelGGL(ce::nn_update_kernel, dim3(a.nchunk_u, a.E), dim3(ce::kNnChunk), 0, s, a);
     hipLaunchKernelGGL(ce::nn_step_kernel, dim3(a.E), dim3(ce::kNnBlock), a.lds_bytes, s, a);
-    if (e->agent_order)
-        hipLaunchKernelGGL(ce::nn_agent_kernel, dim3(a.nchunk, a.E), dim3(ce::kNnChunk), stage, s, a);
-    else
-        hipLaunchKernelGGL(ce::nn_agent_rows_kernel, dim3(a.nchunk, a.E), dim3(ce::kNnChunk), stage, s,
-                           a);
+    hipLaunchKernelGGL(ce::nn_agent_rows_kernel, dim3(a.nchunk, a.E), dim3(ce::kNnChunk), stage, s, a);
     hipLaunchKernelGGL(ce::nn_finalize_kernel, dim3(a.E), dim3(ce::kNnChunk), 0, s, a);
     e->parity ^= 1;
 }
@@ -200,8 +195,7 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     e->P = a.P = static_cast<int>(P);
     e->Ps = static_cast<size_t>((P + 63) & ~63L);
     a.Ps = static_cast<int>(e->Ps);
-    a.nchunk = static_cast<int>((P + ce::kNnChunk * ce::kNnAgentPer - 1) /
-                                (ce::kNnChunk * ce::kNnAgentPer));
+    a.nchunk = static_cast<int>((P + ce::kNnChunk - 1) / ce::kNnChunk);
     a.nchunk_u = static_cast<int>((P + ce::kNnChunk * ce::kNnUpdPer - 1) /
                                   (ce::kNnChunk * ce::kNnUpdPer));
     // LDS: X, every hidden activation, the logits, the split-k scratch
@@ -328,7 +322,6 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     a.epoch_perm = e->epoch_perm;
     a.agent_row = e->agent_row;
     a.row_agent = e->row_agent;
-    if (const char *ag = std::getenv("CE_NN_AGENT")) e->agent_order = std::strcmp(ag, "agent") == 0;
     *out = e;
     return CE_OK;
 }

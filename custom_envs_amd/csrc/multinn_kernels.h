@@ -11,7 +11,7 @@
 //                       (utils_env.py:113-114), theta' = theta - grad * lr
 //   nn_step_kernel      (per env) grad, loss = model.get() at theta'
 //                       (multioptlrs.py:88)
-//   nn_agent_kernel     (per agent) History append, observation v3 ratios,
+//   nn_agent_rows_kernel (per observation row) History append, obs v3 ratios,
 //                       adjusted history, obs = clip(nan_to_num(.), +-100) - 1
 //                       (multioptlrs.py:89-101, utils_env.py:155-161)
 //   nn_finalize_kernel  (per env) reward v6, early stop, the 14 info values
@@ -63,13 +63,8 @@ constexpr int kNnMaxWidth = 512;   // hidden units per layer (multiple of 32)
 constexpr int kNnMaxK = 32;        // classes
 constexpr int kNnMaxH = 16;        // adjusted-history length
 constexpr int kNnPad = 4;          // LDS row padding (floats)
-constexpr int kNnChunk = 256;      // threads (and agents) per block of nn_agent_kernel
+constexpr int kNnChunk = 256;      // threads (and observation rows) per block of nn_agent_rows_kernel
 constexpr int kNnUpdPer = 4;       // agents per thread of nn_update_kernel
-#ifndef CE_NN_AGENT_PER
-#define CE_NN_AGENT_PER 1
-#endif
-constexpr int kNnAgentPer = CE_NN_AGENT_PER;   // agents per thread of nn_agent_kernel
-constexpr int kNnRegH = 8;         // ring ages nn_agent_kernel holds in registers
 constexpr int kNnPrefetch = 8;     // 8-float k-chunks of W in flight per lane
 
 struct NnArgs {
@@ -95,7 +90,7 @@ struct NnArgs {
     float *loss_b;                 // [E] minibatch loss at theta'
     double *part_u;                // [E][nchunk_u][3] update sums (lr, lr^2, reset gradient)
     double *part_c;                // [E][nchunk][5] agent sums (|theta'|, |w~|, |g~|, g, |dg|)
-    int nchunk;                    // nn_agent_kernel blocks per env (kNnChunk * kNnAgentPer agents)
+    int nchunk;                    // nn_agent_rows_kernel blocks per env (kNnChunk rows each)
     int nchunk_u;                  // nn_update_kernel blocks per env
     float *rw, *rg;                // [H][E][Ps] adjusted w~ / g~ entries, obs form
     double *al;                    // [H][E] adjusted loss entries (raw)
@@ -689,133 +684,10 @@ __device__ __forceinline__ NnStepScalars nn_step_scalars(const NnArgs &a, size_t
 }
 
 // History append + observation v3 + adjusted history + obs rows
-// (multioptlrs.py:89-101); on auto-reset theta_n (current next step) <- theta0.
-// kNnAgentPer agents per thread (strided by the block), every agent load
-// issued before the first use.  One agent per thread measured fastest (1.77
-// ms at 1024 envs against 1.82 for two and 2.08 for four: more agents per
-// thread cost occupancy and add staging barriers).  Obs rows go out through an LDS stage, one sub-chunk
-// of kNnChunk agents at a time, as flat (agent, entry) runs so a wave's
-// stores cover consecutive rows (sorted names keep each decade of agents in
-// consecutive rows).
-__global__ __launch_bounds__(kNnChunk) void nn_agent_kernel(NnArgs a) {
-#pragma clang fp contract(off)
-    extern __shared__ float stage[];               // [kNnChunk][3H] obs rows
-    __shared__ int rows_s[kNnChunk];
-    __shared__ float lobs[kNnMaxH];
-    __shared__ double red[(kNnChunk / 64) * 5];
-    const size_t e = blockIdx.y, ps = a.Ps, E = a.E;
-    const int chunk = blockIdx.x, tid = threadIdx.x, H = a.H, W = 3 * H;
-    const int base = chunk * kNnChunk * kNnAgentPer;
-    const NnStepScalars sc = nn_step_scalars(a, e);
-    const int s = sc.s, slot = sc.slot;
-    const size_t plane = E * ps;
-    const float *th_old = a.theta + e * ps, *th_new = a.theta_n + e * ps;
-    const float *gpv = a.gprev + e * ps, *gnv = a.gN + e * ps;
-    const float *rw = a.rw + e * ps, *rg = a.rg + e * ps;
-
-    // ---- every load of the block's agents up front
-    float to[kNnAgentPer], tn[kNnAgentPer], gp[kNnAgentPer], g[kNnAgentPer];
-    float rwv[kNnAgentPer][kNnRegH], rgv[kNnAgentPer][kNnRegH];
-    int row[kNnAgentPer];
-#pragma unroll
-    for (int q = 0; q < kNnAgentPer; ++q) {
-        const int p = base + q * kNnChunk + tid;
-        const int pc = p < a.P ? p : 0;
-        to[q] = th_old[pc];
-        tn[q] = th_new[pc];
-        gp[q] = gpv[pc];
-        g[q] = gnv[pc];
-        row[q] = a.agent_row[pc];
-#pragma unroll
-        for (int k = 1; k < kNnRegH; ++k) {
-            if (k < H && k < s) {                   // block-uniform
-                const size_t sl = ((slot - k) % H + H) % H;
-                rwv[q][k] = rw[sl * plane + pc];
-                rgv[q][k] = rg[sl * plane + pc];
-            } else {
-                rwv[q][k] = rgv[q][k] = -1.0f;      // clip(0) - 1: the reset zeros
-            }
-        }
-    }
-    if (tid < H) {
-        const int k = tid;
-        double lk = 0.0;
-        if (k == 0) lk = sc.adj_l;
-        else if (k < s) lk = a.al[(((slot - k) % H + H) % H) * E + e];
-        lobs[k] = static_cast<float>(clip100(lk) - 1.0);
-    }
-    double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    float *obs = a.obs + e * static_cast<size_t>(a.P) * W;
-    const int dj = kNnChunk / W, dk = kNnChunk - dj * W;   // uniform step of (j, k)
-#pragma unroll
-    for (int q = 0; q < kNnAgentPer; ++q) {
-        const int p0 = base + q * kNnChunk;
-        if (p0 >= a.P) break;                       // block-uniform
-        const int p = p0 + tid;
-        const bool on = p < a.P;
-        const double adj_w = nn_ratio(tn[q], to[q]);
-        const double adj_g = nn_ratio(g[q], gp[q]);
-        const float ow = static_cast<float>(clip100(adj_w) - 1.0);
-        const float og = static_cast<float>(clip100(adj_g) - 1.0);
-        if (on) {
-            v[0] += fabs(static_cast<double>(tn[q]));
-            v[1] += fabs(adj_w);
-            v[2] += fabs(adj_g);
-            v[3] += g[q];
-            v[4] += fabs(static_cast<double>(g[q]) - static_cast<double>(gp[q]));
-            a.rw[slot * plane + e * ps + p] = ow;
-            a.rg[slot * plane + e * ps + p] = og;
-            if (sc.wipe) a.theta_n[e * ps + p] = a.theta0[e * ps + p];
-        }
-        rows_s[tid] = on ? row[q] : -1;
-        __syncthreads();                            // lobs ready; the last sub-chunk's rows are out
-        float *st = stage + tid * W;
-#pragma unroll
-        for (int k = 0; k < kNnRegH; ++k) {
-            if (k < H) {
-                st[k] = sc.wipe ? -1.0f : (k == 0 ? ow : rwv[q][k]);
-                st[H + k] = sc.wipe ? -1.0f : lobs[k];
-                st[2 * H + k] = sc.wipe ? -1.0f : (k == 0 ? og : rgv[q][k]);
-            }
-        }
-        for (int k = kNnRegH; k < H; ++k) {         // long histories: loaded here
-            float wk = -1.0f, gk = -1.0f;
-            if (k < s && on) {
-                const size_t sl = ((slot - k) % H + H) % H;
-                wk = rw[sl * plane + p];
-                gk = rg[sl * plane + p];
-            }
-            st[k] = sc.wipe ? -1.0f : wk;
-            st[H + k] = sc.wipe ? -1.0f : lobs[k];
-            st[2 * H + k] = sc.wipe ? -1.0f : gk;
-        }
-        __syncthreads();
-        const int n = (a.P - p0 < kNnChunk ? a.P - p0 : kNnChunk) * W;
-        int j = tid / W, k = tid - (tid / W) * W;
-#ifdef CE_NN_DIAG_NOOBS
-        if (n < 0)   // timing diagnostic: no observation stores
-#endif
-        for (int f = tid; f < n; f += kNnChunk) {
-            obs[static_cast<size_t>(rows_s[j]) * W + k] = stage[f];
-            j += dj;
-            k += dk;
-            if (k >= W) {
-                k -= W;
-                ++j;
-            }
-        }
-        __syncthreads();
-    }
-    nn_block_sum<5, kNnChunk>(v, red);
-    if (tid == 0) {
-        double *o = a.part_c + (e * a.nchunk + chunk) * 5;
-        for (int k = 0; k < 5; ++k) o[k] = v[k];
-    }
-}
-
-// The same step in OBSERVATION-ROW order (the default; nn_agent_kernel walks
-// agents, CE_NN_AGENT=agent): block = kNnChunk consecutive obs rows of one
-// env, thread = row r, agent p = row_agent[r].
+// (multioptlrs.py:89-101; on auto-reset theta_n <- theta0), in OBSERVATION-ROW
+// order: block = kNnChunk consecutive obs rows of one env, thread = row r,
+// agent p = row_agent[r].  (An agent-order form measured 1.87-1.94 ms at
+// 1024 envs against 1.44 ms for this one)
 //   - The block's observation rows are one contiguous run of kNnChunk * 3H
 //     floats: staged in LDS at the run's 16-byte phase, then written as
 //     float4s (plus at most 3 head and 3 tail floats) instead of 4-byte

@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include "optimize_kernels.h"
 
 namespace ce {
@@ -27,5 +29,8 @@ size_t lr_image_doubles(int n_features, int n_rows);
 void lr_build_image(int n_features, int n_rows, const double *features, const int32_t *labels,
                     double *image);
 void lr_launch_step(const StepArgs<double> &a, hipStream_t stream);
+// The instance lr_launch_step runs for this shape, as rocprof names it:
+// "optimize_lr_mfma_kernel<NKF,MODE,W>"
+std::string lr_kernel_name(int n_envs, int n_rows, int n_features, int lr_waves, int mode_cap);
 
 }  // namespace ce

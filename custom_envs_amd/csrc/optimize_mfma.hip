@@ -47,21 +47,32 @@ struct Table {
 using Gen = Table<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
 static_assert(16 == kGenMaxF / 4, "one instance per k-step count");
 
-// CE_LR_MODE = 0 / 1 / 2 / 3 caps the row-loop mode below what lr_mode(N)
-// allows (experiments; optimize_lr_mfma.h)
-int lr_mode_cap() {
-    static const int cap = [] {
-        const char *m = std::getenv("CE_LR_MODE");
-        return m ? std::atoi(m) : 3;
-    }();
-    return cap;
+// The wave count W and row-loop mode of a launch.  Wave count: 4 waves per
+// workgroup (one per SIMD, tiles 4 at a time, software-pipelined) when every
+// wave gets whole groups of 4 tiles and either the grid fills the chip or
+// there is one group per wave: at 256 x 10, 5.96 us per 4096-env launch
+// against 6.06 at 8 waves and 7.0 at 16, and 5.44 / 5.54 / 6.49 at 1024
+// envs (the row work is the same f64 work at every wave
+// count; more waves cost more in the fixed phases).  Otherwise 8 waves,
+// which halve each wave's rows when a small grid has many of them.
+// lr_waves = 4, 8 or 16 (CE_LR_WAVES at ce_create) forces one.  The mode is
+// lr_mode capped by mode_cap (CE_LR_MODE at ce_create) and by what the wave count is compiled for
+// (4 tiles per group at W <= 4, 2 at W <= 8).
+void lr_choice(int E, int N, int lr_waves, int mode_cap, int *w_out, int *mode_out) {
+    const int groups = (E + kLrEnvs - 1) / kLrEnvs;
+    const int ntiles = (N + 15) / 16;
+    const int w = lr_waves ? lr_waves : lr_mode(N, 4) == 3 && (groups >= 256 || ntiles <= 16) ? 4 : 8;
+    int mode = std::min(lr_mode(N, w), mode_cap);
+    if (mode == 3 && w > 4) mode = 2;
+    if (mode == 2 && w > 8) mode = 1;
+    *w_out = w;
+    *mode_out = mode;
 }
 
 template <int NKF, int W>
-void launch_lr_w(const StepArgs<double> &a, hipStream_t stream) {
+void launch_lr_w(const StepArgs<double> &a, int mode, hipStream_t stream) {
     const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
     const dim3 block(LrShape<W>::kBlock);
-    const int mode = std::min(lr_mode(a.N, W), lr_mode_cap());
     if constexpr (W <= 4) {
         if (mode == 3) {
             hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 3, W>), dim3(grid), block, 0, stream, a);
@@ -80,24 +91,13 @@ void launch_lr_w(const StepArgs<double> &a, hipStream_t stream) {
         hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 0, W>), dim3(grid), block, 0, stream, a);
 }
 
-// Wave count: 4 waves per workgroup (one per SIMD, tiles 4 at a time,
-// software-pipelined) when every wave gets whole groups of 4 tiles and
-// either the grid fills the chip or there is one group per wave: at
-// 256 x 10, 5.96 us per 4096-env launch against 6.06 at 8 waves and 7.0 at
-// 16, and 5.44 / 5.54 / 6.49 at 1024 envs (the row work is
-// the same f64 work at every wave count; more waves cost more in the fixed
-// phases).  Otherwise 8 waves, which halve each wave's rows when a small
-// grid has many of them.  a.lr_waves = 4, 8 or 16 (CE_LR_WAVES at ce_create)
-// forces one.
 template <int NKF>
 void launch_lr(const StepArgs<double> &a, hipStream_t stream) {
-    const int groups = (a.E + kLrEnvs - 1) / kLrEnvs;
-    const int ntiles = (a.N + 15) / 16;
-    const int w = a.lr_waves ? a.lr_waves
-                             : lr_mode(a.N, 4) == 3 && (groups >= 256 || ntiles <= 16) ? 4 : 8;
-    if (w == 16) launch_lr_w<NKF, 16>(a, stream);
-    else if (w == 4) launch_lr_w<NKF, 4>(a, stream);
-    else launch_lr_w<NKF, 8>(a, stream);
+    int w, mode;
+    lr_choice(a.E, a.N, a.lr_waves, a.lr_mode_cap, &w, &mode);
+    if (w == 16) launch_lr_w<NKF, 16>(a, mode, stream);
+    else if (w == 4) launch_lr_w<NKF, 4>(a, mode, stream);
+    else launch_lr_w<NKF, 8>(a, mode, stream);
 }
 constexpr GenFn kLrSteps[4] = {launch_lr<1>, launch_lr<2>, launch_lr<3>, launch_lr<4>};
 
@@ -133,6 +133,13 @@ void lr_build_image(int F, int N, const double *x, const int32_t *y, double *img
 
 void lr_launch_step(const StepArgs<double> &a, hipStream_t stream) {
     kLrSteps[lr_nkf(a.F) - 1](a, stream);
+}
+
+std::string lr_kernel_name(int n_envs, int n_rows, int n_features, int lr_waves, int mode_cap) {
+    int w, mode;
+    lr_choice(n_envs, n_rows, lr_waves, mode_cap, &w, &mode);
+    return "optimize_lr_mfma_kernel<" + std::to_string(lr_nkf(n_features)) + "," +
+           std::to_string(mode) + "," + std::to_string(w) + ">";
 }
 
 int gen_stride_of(int n_features) { return gen_stride(gen_ft(n_features)); }

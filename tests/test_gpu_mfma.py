@@ -25,10 +25,11 @@ def _need_gpu():
 
 
 def _engine(dataset, num_envs, batch_size=None, generic=False, lr=False, lr_waves=0, gen_tail=1,
-            **kw):
+            lr_mode=3, **kw):
     from custom_envs_amd.engine import OptimizeEngine
     flags = {'CE_GENERIC': '1' if generic else '0', 'CE_LR_MFMA': '1' if lr else '0',
-             'CE_LR_WAVES': str(lr_waves), 'CE_GEN_TAIL': str(gen_tail)}
+             'CE_LR_WAVES': str(lr_waves), 'CE_GEN_TAIL': str(gen_tail),
+             'CE_LR_MODE': str(lr_mode)}
     old = {k: os.environ.get(k) for k in flags}
     os.environ.update(flags)
     try:
@@ -211,9 +212,22 @@ def test_lr_mfma_kernel_matches_oracle(n_rows, n_features, num_envs, lr_waves):
     wave count (4 waves: two (env, parameter) roles per thread)."""
     ds = _two_class(n_rows, n_features, n_rows + n_features)
     eng = _engine(ds, num_envs, None, lr=True, lr_waves=lr_waves)
-    assert eng.step_kernel == 'optimize_lr_mfma_kernel<%d>' % ((n_features + 3) // 4)
+    assert eng.step_kernel.startswith('optimize_lr_mfma_kernel<%d,' % ((n_features + 3) // 4))
     envs = sorted({0, num_envs // 2, num_envs - 1})
     _check(ds, None, eng, envs, 43)
+    eng.close()
+
+
+@pytest.mark.parametrize('lr_mode', [0, 1, 2])
+@pytest.mark.parametrize('lr_waves', [4, 8])
+def test_lr_mfma_mode_caps(lr_mode, lr_waves):
+    """CE_LR_MODE caps the row-loop mode below what the shape allows: the
+    benchmark shape (256 x 10) with every tile masked one at a time (0),
+    unmasked one at a time (1) and in pairs (2), at 4 and 8 waves."""
+    ds = _two_class(256, 10, 3)
+    eng = _engine(ds, 35, None, lr=True, lr_waves=lr_waves, lr_mode=lr_mode)
+    assert eng.step_kernel == 'optimize_lr_mfma_kernel<3,%d,%d>' % (lr_mode, lr_waves)
+    _check(ds, None, eng, [0, 16, 34], 42)
     eng.close()
 
 
@@ -251,4 +265,22 @@ def test_two_class_ties_take_class_zero(n_rows, lr):
     eng = _engine((x, y), 19, None, lr=lr)
     assert ('lr_mfma' in eng.step_kernel) == lr
     _check((x, y), None, eng, [0, 9, 18], 12)
+    eng.close()
+
+
+def test_image_shape_full_size():
+    """The reference's default data shape at its real size: load_data('mnist')
+    gives 60,000 rows of 7 x 7 = 49 features and 10 classes, batch_size=None
+    (optimize.py:40, load_data.py:65-71).  The bench's data set
+    (mnist7x7_synthetic), 9 envs (one full 8-env workgroup and a partial
+    one), 42 steps across an auto-reset, against the oracle: the f64
+    gradient sums and the per-lane cross-entropy product folded every 16
+    factors accumulate over all 60,000 rows."""
+    from custom_envs_amd.data import load_data
+    seq = load_data('mnist7x7_synthetic', batch_size=None)
+    ds = (seq.features, seq.targets)
+    assert ds[0].shape == (60000, 49) and ds[1].shape == (60000, 10)
+    eng = _engine(ds, 9, None)
+    assert eng.step_kernel == 'optimize_mfma_kernel<13>'
+    _check(ds, None, eng, [0, 7, 8], 42, scale=0.01)
     eng.close()

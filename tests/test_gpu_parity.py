@@ -208,8 +208,12 @@ def test_single_env_api_matches_oracle(lr_dataset):
     env.close()
 
 
-def test_device_path_matches_host_path(lr_dataset):
+@pytest.mark.parametrize('many_direct', ['32', '0'])
+def test_device_path_matches_host_path(lr_dataset, many_direct, monkeypatch):
+    """ce_step_many as plain launches (k <= CE_MANY_DIRECT, default 32) and
+    as a replayed hipGraph (CE_MANY_DIRECT=0) give the host path's bits."""
     import torch
+    monkeypatch.setenv('CE_MANY_DIRECT', many_direct)
     E, P, K = 512, 20, 12
     acts = np.random.RandomState(4).normal(0, 0.01, (K, E, P)).astype(np.float32)
     host = _engine(lr_dataset, E)
@@ -256,4 +260,46 @@ def test_step_before_reset_is_an_error(lr_dataset):
     eng = _engine(lr_dataset, 4)
     with pytest.raises(NativeEngineError, match='before the first reset'):
         eng.step(np.zeros((4, 20), np.float32))
+    eng.close()
+
+
+def test_benchmark_config_against_live_oracle(lr_dataset):
+    """The bench's own configuration (config 2 as bench.py runs it): 4096
+    envs, 256 x 10, B = N, the default kernel instance (4 waves, row-loop
+    mode 3), seeds 0..4095, actions N(0, 0.01) -- ten envs spread over the
+    grid, the first and last workgroups included (env 4095 is the last lane
+    of the last group), against live oracle envs over 83 steps (two
+    in-kernel auto-resets), plus their float64 weights at the end."""
+    E, P, T = 4096, 20, 83
+    eng = _engine(lr_dataset, E)
+    assert eng.step_kernel == 'optimize_lr_mfma_kernel<3,3,4>'
+    check = [0, 5, 15, 16, 1029, 2047, 2048, 3071, 4080, 4095]
+    seeds = list(range(E))
+    eng.seed(seeds)
+    eng.reset()
+    refs = {}
+    for i in check:
+        env = OracleEnv(*lr_dataset)
+        env.seed(seeds[i])
+        env.reset()
+        refs[i] = env
+    rs = np.random.RandomState(1234)
+    for t in range(T):
+        act = rs.normal(0, 0.01, (E, P)).astype(np.float32)
+        out = eng.step(act)
+        for i, env in refs.items():
+            obs, rew, done, info = env.step(act[i])
+            if done:
+                obs = env.reset()
+            assert bool(out['done'][i]) == done, (i, t)
+            assert out['episode_len'][i] == info['episode']['l'], (i, t)
+            np.testing.assert_allclose(out['obs'][i], obs, rtol=F64_RTOL, atol=F64_ATOL,
+                                       err_msg='env %d step %d' % (i, t))
+            assert out['reward'][i] == pytest.approx(rew, rel=F64_RTOL), (i, t)
+            assert out['objective'][i] == pytest.approx(info['objective'], rel=F64_RTOL), (i, t)
+            assert out['accuracy'][i] == np.float32(info['accuracy']), (i, t)
+    st = eng.get_state()
+    for i, env in refs.items():
+        np.testing.assert_allclose(st['weights'][i], env.model.weights.ravel(), rtol=1e-12,
+                                   atol=1e-14)
     eng.close()

@@ -41,13 +41,17 @@ def _dataset(n_features, n_rows=200, seed=3):
     return x, np.eye(2)[y]
 
 
-def _rollout(dataset, pair_u, num_envs, batch_size, steps=43, precision='f64'):
+def _rollout(dataset, pair_u, num_envs, batch_size, steps=43, precision='f64', flags=None,
+             kernel=None):
     from custom_envs_amd.engine import OptimizeEngine
-    saved = {k: os.environ.get(k) for k in ('CE_PAIR_U',)}
-    os.environ['CE_PAIR_U'] = str(pair_u)
+    flags = dict(flags or {}, CE_PAIR_U=str(pair_u))
+    saved = {k: os.environ.get(k) for k in flags}
+    os.environ.update(flags)
     try:
         eng = OptimizeEngine(*dataset, num_envs=num_envs, batch_size=batch_size,
                              precision=precision)
+        if kernel is not None:
+            assert eng.step_kernel == kernel
     finally:
         for k, v in saved.items():
             if v is None:
@@ -192,4 +196,20 @@ def test_general_k_softmax(shape, batch_size, precision):
     ds = _multiclass(*shape)
     E = 21
     seeds, acts, outs = _rollout(ds, 0, E, batch_size, precision=precision)
+    _check_against_oracle(ds, batch_size, seeds, acts, outs, [0, 10, 20], precision=precision)
+
+
+@pytest.mark.parametrize('precision', ['f64', 'f32'])
+@pytest.mark.parametrize('batch_size', [None, 32])
+@pytest.mark.parametrize('shape', [(10, 2), (10, 3)])
+def test_unstaged_register_kernel(shape, batch_size, precision):
+    """CE_NO_STAGE=1: the one-env-per-wave kernel reading rows from L1/L2
+    instead of the LDS stage (the path data sets too large for the stage
+    take) against the oracle, two-class and general K."""
+    ds = _multiclass(*shape) if shape[1] > 2 else _dataset(10)
+    E = 21
+    dt = 'double' if precision == 'f64' else 'float'
+    seeds, acts, outs = _rollout(ds, 2, E, batch_size, precision=precision,
+                                 flags={'CE_NO_STAGE': '1'},
+                                 kernel='optimize_step_kernel<%s,%d,%d,false>' % (dt, *shape))
     _check_against_oracle(ds, batch_size, seeds, acts, outs, [0, 10, 20], precision=precision)
