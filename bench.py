@@ -531,8 +531,11 @@ def main():
         dry_run(args, world, rank)
         return 0
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
-        cpu = run_cpu_baseline_child(args)     # before this process touches the GPU
+    if rank == 0 and not args.no_cpu_baseline and not args.profile_only:
+        # every N: the reference path on the same box's host cores, in the
+        # same run (north_star); a child process started before this rank
+        # touches the GPU, while the other ranks wait in the rendezvous
+        cpu = run_cpu_baseline_child(args)
 
     import torch
     dist = None

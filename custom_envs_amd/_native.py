@@ -27,7 +27,7 @@ STATUS_NAMES = {CE_EINVAL: 'CE_EINVAL', CE_EHIP: 'CE_EHIP', CE_ENOMEM: 'CE_ENOME
 # Every symbol include/custom_envs_amd.h declares.
 EXPORTS = (
     'ce_abi_version', 'ce_last_error', 'ce_create', 'ce_destroy', 'ce_set_stream',
-    'ce_num_envs', 'ce_obs_dim', 'ce_act_dim', 'ce_seed', 'ce_seed_draws',
+    'ce_set_compact_outputs', 'ce_num_envs', 'ce_obs_dim', 'ce_act_dim', 'ce_seed', 'ce_seed_draws',
     'ce_seed_draws_mlp', 'ce_reset',
     'ce_step', 'ce_step_async', 'ce_wait', 'ce_step_many', 'ce_step_many_prepare',
     'ce_host_outputs', 'ce_step_kernel',
@@ -103,6 +103,7 @@ def _declare(lib):
         'ce_create': ([ctypes.POINTER(CeConfig), vp, vp, ctypes.POINTER(vp)], ctypes.c_int),
         'ce_destroy': ([vp], None),
         'ce_set_stream': ([vp, vp], ctypes.c_int),
+        'ce_set_compact_outputs': ([vp, i32], ctypes.c_int),
         'ce_num_envs': ([vp], ctypes.c_int),
         'ce_obs_dim': ([vp], ctypes.c_int),
         'ce_act_dim': ([vp], ctypes.c_int),

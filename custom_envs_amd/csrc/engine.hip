@@ -128,6 +128,7 @@ struct ce_engine {
     int lr_waves = 0;         // CE_LR_WAVES: force the two-class MFMA kernel's wave count
     int gen_tail = 1;         // CE_GEN_TAIL=0: the runtime-shape kernel's last feature on MFMA too
     int lr_mode_cap = 3;      // CE_LR_MODE: cap on the two-class MFMA kernel's row-loop mode
+    bool compact = false;     // ce_set_compact_outputs: device-pointer calls write the compact form
     unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
 };
 
@@ -145,7 +146,8 @@ ce_outputs region_view(const ce_engine *e, char *base) {
 }
 
 template <typename T>
-ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs &o) {
+ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs &o,
+                          bool compact = false) {
     ce::StepArgs<T> a;
     a.E = e->cfg.num_envs;
     a.N = e->cfg.n_rows;
@@ -177,6 +179,8 @@ ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs
     a.lr_waves = e->lr_waves;
     a.gen_tail = e->gen_tail;
     a.lr_mode_cap = e->lr_mode_cap;
+    a.obs_stride = compact ? P + 1 : 2 * P + 1;
+    a.obs_lo = compact ? P : 0;
     return a;
 }
 
@@ -215,8 +219,10 @@ ce::MlpArgs make_mlp_args(const ce_engine *e, const float *act, const ce_outputs
     return a;
 }
 
+// compact: the caller's device outputs are in the compact form
+// (ce_set_compact_outputs; only the two-class MFMA path writes it)
 void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &o,
-            hipStream_t stream) {
+            hipStream_t stream, bool compact = false) {
     if (e->mlp) {
         const ce::MlpArgs a = make_mlp_args(e, act, o);
         const dim3 grid(e->cfg.num_envs), block(ce::kMlpBlock);
@@ -239,7 +245,7 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
         return;
     }
     if (e->lr_mfma) {
-        auto a = make_args<double>(e, act, o);
+        auto a = make_args<double>(e, act, o, compact);
         if (reset)
             ce::gen_launch_reset(a, stream);
         else
@@ -268,7 +274,7 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
 // k steps of every env, actions s * stride apart.
 void launch_steps(const ce_engine *e, int k, const float *actions, int64_t stride,
                   const ce_outputs &o) {
-    for (int s = 0; s < k; ++s) launch(e, false, actions + s * stride, o, e->stream);
+    for (int s = 0; s < k; ++s) launch(e, false, actions + s * stride, o, e->stream, e->compact);
 }
 
 // Convert host float64 values to a device array of `elem`-byte floats.
@@ -310,8 +316,10 @@ void copy_out(const ce_engine *e, const ce_outputs &src, const ce_outputs *dst) 
     if (dst->episode_len) std::memcpy(dst->episode_len, src.episode_len, E * sizeof(int32_t));
 }
 
-bool complete(const ce_outputs *o) {
-    return o && o->obs && o->reward && o->done && o->objective && o->accuracy && o->episode_len;
+// every output pointer set (the compact form may leave done null)
+bool complete(const ce_outputs *o, bool compact = false) {
+    return o && o->obs && o->reward && (o->done || compact) && o->objective && o->accuracy &&
+           o->episode_len;
 }
 
 int do_step(ce_engine *e, const float *actions, const ce_outputs *out, uint32_t flags,
@@ -321,9 +329,10 @@ int do_step(ce_engine *e, const float *actions, const ce_outputs *out, uint32_t 
     if (!actions) return fail(CE_EINVAL, "null actions");
     const size_t E = e->cfg.num_envs;
     if (flags & CE_PTR_DEVICE) {
+        if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
         ce_outputs o = out ? *out : region_view(e, e->d_out);
-        if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
-        launch(e, false, actions, o, e->stream);
+        if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
+        launch(e, false, actions, o, e->stream, e->compact);
         CE_HIP(hipGetLastError());
         if (sync) CE_HIP(hipStreamSynchronize(e->stream));
         return CE_OK;
@@ -637,6 +646,17 @@ int ce_set_stream(ce_engine *e, void *stream) {
     return CE_OK;
 }
 
+int ce_set_compact_outputs(ce_engine *e, int32_t on) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    if (on && !e->lr_mfma)
+        return fail(CE_EUNSUPPORTED, "ce_set_compact_outputs: only the two-class full-batch "
+                                     "float64 kernel (" + std::string("optimize_lr_mfma_kernel") +
+                                     ") writes the compact form; this engine runs " + e->kernel_name);
+    if (e->compact != (on != 0)) e->graphs.release();   // captured launches carry the form
+    e->compact = on != 0;
+    return CE_OK;
+}
+
 int ce_num_envs(const ce_engine *e) { return e ? e->cfg.num_envs : CE_EINVAL; }
 int ce_obs_dim(const ce_engine *e) { return e ? e->obs_dim : CE_EINVAL; }
 int ce_act_dim(const ce_engine *e) { return e ? e->P : CE_EINVAL; }
@@ -684,9 +704,10 @@ int ce_seed(ce_engine *e, const uint64_t *seeds, int32_t n) {
 int ce_reset(ce_engine *e, const ce_outputs *out, uint32_t flags) {
     if (!e) return fail(CE_EINVAL, "null engine");
     if (flags & CE_PTR_DEVICE) {
-        if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+        if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
+        if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
         ce_outputs o = out ? *out : region_view(e, e->d_out);
-        launch(e, true, nullptr, o, e->stream);
+        launch(e, true, nullptr, o, e->stream, e->compact);
         CE_HIP(hipGetLastError());
         e->was_reset = true;
         return CE_OK;
@@ -723,7 +744,8 @@ int many_graph(ce_engine *e, int32_t k, const float *actions, int64_t stride,
     if (!e) return fail(CE_EINVAL, "null engine");
     if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
     if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "ce_step_many: bad arguments");
-    if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+    if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
+    if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
     const ce_outputs o = out ? *out : region_view(e, e->d_out);
     return e->graphs.get(ce::graph_key(k, 0, actions, stride, e->stream, o), [&] {
         launch_steps(e, k, actions, stride, o);
@@ -737,7 +759,8 @@ int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
     if (e && k <= e->many_direct) {
         if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
         if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "ce_step_many: bad arguments");
-        if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+        if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
+        if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
         const ce_outputs o = out ? *out : region_view(e, e->d_out);
         launch_steps(e, k, actions, stride, o);
         CE_HIP(hipGetLastError());

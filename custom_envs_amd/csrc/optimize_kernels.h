@@ -95,6 +95,9 @@ struct StepArgs {
     int lr_waves;               // two-class MFMA kernel: 0 = pick per launch, 4 / 8 = forced
     int gen_tail;               // runtime-shape MFMA kernel: last feature on the VALU when F % 16 == 1
     int lr_mode_cap;            // two-class MFMA kernel: cap on the row-loop mode (3 = none)
+    int obs_stride;             // floats per obs row: 2P + 1, or P + 1 in the compact form
+    int obs_lo;                 // first obs entry stored: 0, or P (compact: the wght_hist
+                                // block is identically 0 and not stored; done may be null)
 };
 
 // Diagnostic builds (-DCE_DIAG) stamp s_memtime at phase boundaries into a

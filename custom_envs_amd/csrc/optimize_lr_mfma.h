@@ -167,7 +167,10 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, h = lane >> 4;
-    const int F = a.F, P = 2 * F, N = a.N, B = a.B, OBS = 2 * P + 1;
+    const int F = a.F, P = 2 * F, N = a.N, B = a.B;
+    // observation rows: obs_stride floats per env from entry obs_lo on (the
+    // compact form, obs_lo = P, leaves out the identically-zero weight block)
+    const int OS = a.obs_stride, OL = a.obs_lo;
     const int e0 = blockIdx.x * kLrEnvs;
     const int e = e0 + c;                               // this lane's env (columns)
     const bool env_ok = e < a.E;
@@ -414,9 +417,9 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     // episode length
 #pragma unroll
     for (int r = 0; r < PR; ++r)
-        if (prole[r]) a.obs[static_cast<unsigned>(e0 + pj[r]) * OBS + pp[r]] = 0.0f;
+        if (prole[r] && OL == 0) a.obs[static_cast<unsigned>(e0 + pj[r]) * OS + pp[r]] = 0.0f;
     if (srole) {
-        a.done[es] = cur >= a.max_steps ? 1 : 0;
+        if (a.done) a.done[es] = cur >= a.max_steps ? 1 : 0;
         a.episode_len[es] = cur;
     }
     // partials of this wave: s (features h + 4r of env c); -log of the
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
         a.reward[es] = static_cast<float>(-loss);
         a.objective[es] = static_cast<float>(loss);     // B == N: the same numbers
         a.accuracy[es] = static_cast<float>(acc);
-        a.obs[es * OBS + P] = wipe ? 0.0f : static_cast<float>(lnew);
+        a.obs[es * OS + P - OL] = wipe ? 0.0f : static_cast<float>(lnew);
         a.L[es] = wipe ? 0.0 : lnew;
         a.step[es] = wipe ? 0 : cur;
     }
@@ -475,7 +478,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
         for (int w = 0; w < kLrWaves; ++w) sf += red_s[w][f >> 2][pj[r] + 16 * (f & 3)];
         const double g = div_rcp((pp[r] & 1) ? sf : -sf, dB, rB);
         const double gnew = div_rcp(g, fabs(g_prev[r]) + 1.0, rG[r]);
-        a.obs[static_cast<unsigned>(e0 + pj[r]) * OBS + P + 1 + pp[r]] =
+        a.obs[static_cast<unsigned>(e0 + pj[r]) * OS + P + 1 + pp[r] - OL] =
             wipe ? 0.0f : static_cast<float>(gnew);
         a.W[gi[r]] = wipe ? w_init[r] : wsh[pj[r]][pp[r]];
         a.G[gi[r]] = wipe ? 0.0 : gnew;

@@ -203,8 +203,9 @@ __global__ __launch_bounds__(kWave *kGenResetWaves) void optimize_reset_rt_kerne
     if (e >= a.E) return;
     const int P = a.F * a.K;
     reset_env_rt(a, e, lane, P);
-    float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
-    for (int i = lane; i < 2 * P + 1; i += kWave) obs[i] = 0.0f;
+    (void)P;
+    float *obs = a.obs + static_cast<size_t>(e) * a.obs_stride;   // full or compact row
+    for (int i = lane; i < a.obs_stride; i += kWave) obs[i] = 0.0f;
 }
 
 // Z^T = sum over k of W'^T_k X^T_k as kGenChains independent accumulator

@@ -94,25 +94,46 @@ class GatheredOutputs(Mapping):
     ``rank_major[name]`` is a zero-copy (world, capacity * rows, ...) view of
     the collective's buffer.  ``outputs[name]`` is the global array in env
     order, built on first access (one copy per field, only for fields a
-    consumer reads)."""
+    consumer reads; at world 1 a zero-copy view).  ``derived`` names fields
+    the wire format leaves out (the compact form: full ``obs`` rows and
+    ``done``) with the function that rebuilds each from the stored fields.
 
-    def __init__(self, layout, gathered, counts):
+    Lifetime: the result reads the slot's gather buffer.  The next gather into
+    the same slot overwrites it, so a field first read after that returns the
+    newer step's data.  Read what you need before then, or call
+    ``snapshot()``, which materialises every field as its own tensor.
+    """
+
+    def __init__(self, layout, gathered, counts, derived=None):
         self.layout, self.counts = layout, counts
         self.rank_major = layout.rank_views(gathered, len(counts))
         self._rows = {name: r for name, _, r, _ in layout.fields}
+        self._derived = dict(derived or {})
         self._flat = {}
 
     def __getitem__(self, name):
         if name not in self._flat:
-            v, rows = self.rank_major[name], self._rows[name]
-            self._flat[name] = torch.cat([v[r, :c * rows] for r, c in enumerate(self.counts)])
+            if name in self._derived:
+                self._flat[name] = self._derived[name](self)
+            else:
+                v, rows = self.rank_major[name], self._rows[name]
+                if len(self.counts) == 1:
+                    self._flat[name] = v[0, :self.counts[0] * rows]
+                else:
+                    self._flat[name] = torch.cat([v[r, :c * rows] for r, c in enumerate(self.counts)])
         return self._flat[name]
 
     def __iter__(self):
-        return iter(self.rank_major)
+        names = list(self.rank_major)
+        return iter(names + [n for n in self._derived if n not in names])
 
     def __len__(self):
-        return len(self.rank_major)
+        return len(set(self.rank_major) | set(self._derived))
+
+    def snapshot(self):
+        """Every field (stored and derived) as a tensor of its own: valid after
+        later gathers into the same slot."""
+        return {name: self[name].clone() for name in self}
 
 
 class ShardedEnvs:
@@ -127,9 +148,14 @@ class ShardedEnvs:
     """
 
     def __init__(self, engine, num_envs, rank=0, world=1, group=None, device=None, slots=1,
-                 collective=None):
+                 collective=None, compact=None):
         """``collective``: run the all-gather even at world 1 (tests the RCCL
-        path on one GPU); default: only when world > 1."""
+        path on one GPU); default: only when world > 1.  ``compact``: have the
+        engine write (and the collective move) the compact record -- obs
+        without its identically-zero weight block, done folded into
+        episode_len -- when the engine offers it (``set_compact_outputs``);
+        default: whenever the collective runs.  ``gather`` rebuilds the full
+        fields lazily."""
         self.engine, self.rank, self.world, self.group = engine, rank, world, group
         self.collective = world > 1 if collective is None else bool(collective)
         self.num_envs = int(num_envs)
@@ -139,6 +165,17 @@ class ShardedEnvs:
                              % (engine.num_envs, rank, self.hi - self.lo))
         self.counts = [b - a for a, b in (shard_range(self.num_envs, world, r)
                                           for r in range(world))]
+        if compact is None:
+            compact = self.collective
+        self.compact = False
+        if compact and hasattr(engine, 'set_compact_outputs'):
+            from custom_envs_amd._native import NativeEngineError
+            try:
+                engine.set_compact_outputs(True)
+                self.compact = True
+            except NativeEngineError:       # this engine's kernel writes the full form only
+                pass
+        self.derived = engine.derived_fields() if hasattr(engine, 'derived_fields') else {}
         self.layout = PackedLayout(engine.output_fields(), max(self.counts))
         device = device if device is not None else torch.device('cuda', torch.cuda.current_device())
         self.buffers = [torch.zeros(self.layout.nbytes, dtype=torch.uint8, device=device)
@@ -173,13 +210,16 @@ class ShardedEnvs:
 
     def gather(self, slot=0, async_op=False):
         """Every rank gets the global outputs: ONE all_gather_into_tensor of the
-        packed buffer.  Returns ``GatheredOutputs`` (or this rank's outputs at
-        world 1); with ``async_op`` also the collective's work handle, whose
-        ``wait()`` orders the caller's current stream after it."""
+        packed buffer.  Returns ``GatheredOutputs`` (at world 1 without the
+        collective, views of this rank's own buffer); with ``async_op`` also the
+        collective's work handle, whose ``wait()`` orders the caller's current
+        stream after it."""
         if not self.collective:
-            return (self.outs[slot], None) if async_op else self.outs[slot]
+            res = GatheredOutputs(self.layout, self.buffers[slot], [self.hi - self.lo],
+                                  self.derived)
+            return (res, None) if async_op else res
         import torch.distributed as dist
         work = dist.all_gather_into_tensor(self.gathered[slot], self.buffers[slot],
                                            group=self.group, async_op=async_op)
-        res = GatheredOutputs(self.layout, self.gathered[slot], self.counts)
+        res = GatheredOutputs(self.layout, self.gathered[slot], self.counts, self.derived)
         return (res, work) if async_op else res

@@ -43,6 +43,22 @@ def _view(ptr, count, ctype, dtype, shape):
     return np.frombuffer(buf, dtype=dtype).reshape(shape)
 
 
+def compact_derived(n_params, max_steps):
+    """The full obs rows and the done flags from the compact fields."""
+    import torch
+
+    def obs(f):
+        tail = f['obs_tail']
+        full = torch.zeros((tail.shape[0], 2 * n_params + 1), dtype=tail.dtype, device=tail.device)
+        full[:, n_params:] = tail
+        return full
+
+    def done(f):
+        return (f['episode_len'] >= max_steps).to(torch.uint8)
+
+    return {'obs': obs, 'done': done}
+
+
 class OptimizeEngine:
     """E Optimize-v0 environments advanced in lock step on one GPU."""
 
@@ -96,6 +112,7 @@ class OptimizeEngine:
             'episode_len': _view(view.episode_len, E, ctypes.c_int32, np.int32, (E,)),
         }
         self.seeds = [None] * E
+        self.compact = False
 
     # ------------------------------------------------------------------ seeding
     def seed(self, seeds):
@@ -140,20 +157,46 @@ class OptimizeEngine:
 
     @staticmethod
     def _outputs(out):
-        return CeOutputs(obs=out['obs'].data_ptr(), reward=out['reward'].data_ptr(),
-                         done=out['done'].data_ptr(), objective=out['objective'].data_ptr(),
+        obs = out['obs_tail'] if 'obs_tail' in out else out['obs']
+        return CeOutputs(obs=obs.data_ptr(), reward=out['reward'].data_ptr(),
+                         done=out['done'].data_ptr() if 'done' in out else None,
+                         objective=out['objective'].data_ptr(),
                          accuracy=out['accuracy'].data_ptr(),
                          episode_len=out['episode_len'].data_ptr())
 
+    def set_compact_outputs(self, on=True):
+        """Device-pointer calls write the compact form (``ce_set_compact_outputs``):
+        ``obs_tail`` = obs[:, P:] (the wght_hist block obs[:, :P] is
+        identically 0, optimize.py:84-86) and no ``done`` (done == episode_len
+        >= max_steps).  ``derived_fields`` rebuilds both.  Raises
+        ``NativeEngineError`` (CE_EUNSUPPORTED) unless this engine runs the
+        two-class full-batch float64 kernel."""
+        check(self._lib.ce_set_compact_outputs(self._h, 1 if on else 0), 'ce_set_compact_outputs')
+        self.compact = bool(on)
+
     def output_fields(self):
-        """(name, torch dtype, rows per env, trailing shape) of the step outputs."""
+        """(name, torch dtype, rows per env, trailing shape) of the step outputs
+        as the engine writes them (full or compact form)."""
         import torch
+        if self.compact:
+            return [('obs_tail', torch.float32, 1, (self.act_dim + 1,)),
+                    ('reward', torch.float32, 1, ()),
+                    ('objective', torch.float32, 1, ()),
+                    ('accuracy', torch.float32, 1, ()),
+                    ('episode_len', torch.int32, 1, ())]
         return [('obs', torch.float32, 1, (self.obs_dim,)),
                 ('reward', torch.float32, 1, ()),
                 ('done', torch.uint8, 1, ()),
                 ('objective', torch.float32, 1, ()),
                 ('accuracy', torch.float32, 1, ()),
                 ('episode_len', torch.int32, 1, ())]
+
+    def derived_fields(self):
+        """Fields the compact form leaves out, as functions of the fields it
+        stores (name -> fn(fields) -> tensor): the full obs rows and done."""
+        if not self.compact:
+            return {}
+        return compact_derived(self.act_dim, self.max_steps)
 
     def alloc_device_outputs(self, torch_device=None):
         import torch
@@ -169,7 +212,10 @@ class OptimizeEngine:
         for key, t in out.items():
             if not t.is_contiguous():
                 raise ValueError('output %s must be contiguous' % key)
-        if out['obs'].numel() != self.num_envs * self.obs_dim:
+        if self.compact:
+            if 'obs_tail' not in out or out['obs_tail'].numel() != self.num_envs * (self.act_dim + 1):
+                raise ValueError('compact outputs need obs_tail of [E][P + 1]')
+        elif 'obs' not in out or out['obs'].numel() != self.num_envs * self.obs_dim:
             raise ValueError('obs output has the wrong size')
 
     def reset_device(self, out):

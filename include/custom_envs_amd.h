@@ -156,6 +156,16 @@ int ce_create(const ce_config *cfg, const double *features /* [N][F] */,
 void ce_destroy(ce_engine *eng);
 
 int ce_set_stream(ce_engine *eng, void *hip_stream /* NULL: engine's own */);
+/* Compact output form for the per-step all-gather (SURVEY 8e, config 4;
+ * replaces nothing in the reference, whose VecEnv np.stacks full obs rows,
+ * concurrentvecenv.py:99-104).  When on, every CE_PTR_DEVICE call and
+ * ce_step_many writes obs as [E][P + 1] = (loss_hist[idx], grad_hist[idx])
+ * only -- the wght_hist block of the observation is identically 0
+ * (optimize.py:84-86) and is not stored -- and `done` may be NULL
+ * (done == episode_len >= max_steps).  Host-mode calls keep the full form.
+ * CE_EUNSUPPORTED unless the engine runs the two-class full-batch float64
+ * kernel (ce_step_kernel "optimize_lr_mfma_kernel<...>"). */
+int ce_set_compact_outputs(ce_engine *eng, int32_t on);
 int ce_num_envs(const ce_engine *eng);
 int ce_obs_dim(const ce_engine *eng);
 int ce_act_dim(const ce_engine *eng);

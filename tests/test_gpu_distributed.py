@@ -56,8 +56,11 @@ def _oracle_rows(features, targets, seeds, acts):
     return rows
 
 
+@pytest.mark.parametrize('compact', [True, False])
 @pytest.mark.parametrize('pipelined', [False, True])
-def test_sharded_engine_gather_matches_oracle(nccl_world1, lr_dataset, pipelined):
+def test_sharded_engine_gather_matches_oracle(nccl_world1, lr_dataset, pipelined, compact):
+    """compact (the default when the collective runs): the engine writes
+    obs[P:] and no done; the gathered view rebuilds both."""
     import torch
     from custom_envs_amd.distributed import ShardedEnvs
     from custom_envs_amd.engine import OptimizeEngine
@@ -67,12 +70,15 @@ def test_sharded_engine_gather_matches_oracle(nccl_world1, lr_dataset, pipelined
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
-    shard = ShardedEnvs(eng, E, 0, 1, slots=2, collective=True)
-    # packed segments: every field 256-B aligned, obs rows [E][41]
+    shard = ShardedEnvs(eng, E, 0, 1, slots=2, collective=True, compact=compact)
+    assert shard.compact == compact and eng.compact == compact
+    # packed segments: every field 256-B aligned, obs rows [E][41] (compact: [E][21])
+    obs_key, width = ('obs_tail', 21) if compact else ('obs', 41)
     assert all(off % 256 == 0 for off in shard.layout.offsets.values())
-    assert shard.outs[0]['obs'].shape == (E, 41)
-    assert shard.outs[0]['obs'].data_ptr() == shard.buffers[0].data_ptr() + \
-        shard.layout.offsets['obs']
+    assert shard.outs[0][obs_key].shape == (E, width)
+    assert shard.outs[0][obs_key].data_ptr() == shard.buffers[0].data_ptr() + \
+        shard.layout.offsets[obs_key]
+    assert ('done' in shard.outs[0]) != compact
     shard.seed(base)
     shard.reset(0)
     acts = np.random.RandomState(8).normal(0, 0.02, (steps, E, 20)).astype(np.float32)
@@ -84,7 +90,7 @@ def test_sharded_engine_gather_matches_oracle(nccl_world1, lr_dataset, pipelined
     def collect(entry):
         work, res, t = entry
         work.wait()              # the current stream waits for the collective
-        assert res.rank_major['obs'].shape == (1, E, 41)   # zero-copy view
+        assert res.rank_major[obs_key].shape == (1, E, width)   # zero-copy view
         got[t] = {k: res[k].cpu().numpy() for k in keys}
 
     for t in range(steps):
@@ -111,3 +117,69 @@ def test_sharded_engine_gather_matches_oracle(nccl_world1, lr_dataset, pipelined
         np.testing.assert_allclose(g['reward'], e['reward'], rtol=1e-6)
     eng.close()
     torch.cuda.set_stream(torch.cuda.default_stream())
+
+
+def test_compact_outputs_need_the_two_class_kernel(lr_dataset):
+    """Only the two-class full-batch float64 kernel writes the compact form."""
+    from custom_envs_amd import NativeEngineError
+    from custom_envs_amd.engine import OptimizeEngine
+    features, targets = lr_dataset
+    eng = OptimizeEngine(features, targets, num_envs=4, batch_size=32)
+    with pytest.raises(NativeEngineError, match='compact'):
+        eng.set_compact_outputs(True)
+    eng.close()
+
+
+def test_sharded_multiagent_gather_matches_oracle(nccl_world1):
+    """Config 5 (run_multiagent_exp_single.py:37,78-86): MultiOptEngine
+    (4 agents, 4-D Rosenbrock pairs, H = 5) driven through ShardedEnvs with a
+    real RCCL all-gather at world 1, against oracle OptEnvRunners: done and
+    episode length exact, obs rows and reward within float32 rounding,
+    info within 1e-5 (tolerances of test_gpu_multi.py)."""
+    import torch
+    from custom_envs_amd._native import MULTI_INFO_KEYS
+    from custom_envs_amd.distributed import ShardedEnvs
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    from oracle.multioptlrs import MultiOptLRs as OracleMulti, OptEnvRunner
+    E, P, H, MB, T = 13, 4, 5, 30, 45
+    rs = np.random.RandomState(12)
+    lows = rs.uniform(-1.5, 1.5, E)
+    acts = np.stack([rs.uniform(lows[e], lows[e] + 1.5, (T, P)) for e in range(E)], 1)
+    acts = acts.astype(np.float32).reshape(T, E * P)
+    eng = MultiOptEngine(E, 'func4', max_batches=MB, max_history=H)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    eng.set_stream(stream.cuda_stream)
+    shard = ShardedEnvs(eng, E, 0, 1, collective=True)
+    refs = [OptEnvRunner(OracleMulti(P, max_batches=MB, max_history=H)) for _ in range(E)]
+    dacts = torch.from_numpy(acts).cuda()
+    try:
+        shard.reset()
+        first = shard.gather()['obs'].cpu().numpy()
+        assert np.array_equal(first, np.concatenate([np.stack(r.reset()) for r in refs]))
+        for t in range(T):
+            shard.step(dacts[t])
+            g = shard.gather().snapshot()
+            torch.cuda.synchronize()
+            g = {k: v.cpu().numpy() for k, v in g.items()}
+            for e, runner in enumerate(refs):
+                states, rewards, dones, infos = runner.step(list(acts[t, e * P:(e + 1) * P].reshape(P, 1)))
+                if dones[0]:
+                    states = runner.reset()
+                rows = slice(e * P, (e + 1) * P)
+                assert np.all(g['done'][rows] == dones[0]), (t, e)
+                assert int(g['episode_len'][e]) == infos[0]['episode']['l'], (t, e)
+                ref = np.stack(states).astype(np.float64)
+                scale = np.maximum(np.abs(ref).max(axis=-1), 1.0)
+                assert np.all(np.abs(g['obs'][rows] - ref).max(axis=-1) / scale <= 1e-6), (t, e)
+                assert abs(g['reward'][e * P] - rewards[0]) <= 1e-6 * max(1.0, abs(rewards[0]))
+                ref_info = np.array([np.nan if infos[0][k] is None else float(infos[0][k])
+                                     for k in MULTI_INFO_KEYS])
+                fin = np.isfinite(ref_info) & (np.arange(len(ref_info)) != 8) & \
+                    (np.arange(len(ref_info)) != 9)     # signed gradient sums: test_gpu_multi.py
+                assert np.array_equal(np.isnan(g['info'][e]), np.isnan(ref_info)), (t, e)
+                err = np.abs(g['info'][e][fin] - ref_info[fin]) / np.maximum(np.abs(ref_info[fin]), 1e-6)
+                assert np.all(err <= 1e-5), (t, e, err.max())
+    finally:
+        eng.close()
+        torch.cuda.set_stream(torch.cuda.default_stream())
