@@ -16,15 +16,18 @@ child process before anything touches a GPU; under torchrun (the driver's
 launch) the ranks come from RANK/WORLD_SIZE.
 
 Multi-GPU (config 4).  Every step all-gathers the packed outputs of every
-rank (custom_envs_amd/distributed.py: ONE all_gather_into_tensor of a
-256-B-aligned [obs|reward|done|objective|accuracy|len] record per env,
-RCCL over xGMI).  ``value`` is the pipelined form: two output buffers, the
-collective of step t runs on RCCL's stream while step t+1's kernel writes
-the other buffer (the learner consumes step t's global outputs one step
-behind the envs).  The line also carries ``value_gather_serial`` (kernel,
-then the collective, every step: a closed-loop learner) and
-``value_no_gather`` (the env kernels alone, hipGraph replay).  At N = 1 the
-gather is the identity and ``value`` is the hipGraph replay of S steps.
+rank (custom_envs_amd/distributed.py: ONE all_gather_into_tensor of the
+compact per-env record [obs without its identically-zero weight block |
+reward | objective | accuracy | episode_len] in 256-B-aligned segments,
+RCCL over xGMI; done is episode_len >= 40 and the full obs rows are
+rebuilt lazily on the consumer).  ``value`` is the SERIAL schedule: the
+step kernel, then the collective, every step -- what a closed-loop learner
+consumes.  The line also carries ``value_gather_pipelined`` (two output
+buffers, the collective of step t on RCCL's stream while step t+1's kernel
+writes the other buffer: an open-loop consumer one step behind) and
+``value_no_gather`` (the env kernels alone, hipGraph replay).  At N = 1
+(without --force-gather) there is no collective and ``value`` is the
+hipGraph replay of S steps.
 
 ``--workload multi`` measures config 5 instead: MultiOptLRs-v0 (4 agents,
 4-D Rosenbrock pairs, H=5, max_batches=400) behind OptVecEnv, 1024 envs per
@@ -668,10 +671,9 @@ def main():
         run_graph(args.warmup)
         modes['no_gather'] = _timed(torch, dist, run_graph, args.steps)
         # both schedules run every step AND its all-gather inside the timed
-        # region; `value` is the faster of the two (at world 1 the pipelined
-        # one's cross-stream waits cost more than the copy it hides: 14.2 vs
-        # 7.7 us per step, profiles/r02_bench_force_gather.json)
-        gather_mode = min(('pipelined', 'serial'), key=lambda m: modes[m])
+        # region; `value` is the closed-loop serial one (a learner acts on
+        # step t's outputs before step t + 1), the pipelined rate rides along
+        gather_mode = 'serial'
         elapsed = modes[gather_mode]
     else:
         primary = run_graph
@@ -735,9 +737,11 @@ def main():
         if modes:
             units = world * E * args.steps
             line['value_gather_serial'] = units / modes['serial']
+            line['value_gather_pipelined'] = units / modes['pipelined']
             line['value_no_gather'] = units / modes['no_gather']
             line['ms_per_step_modes'] = {k: v / args.steps * 1e3 for k, v in modes.items()}
             line['gather_bytes_per_rank'] = shard.layout.nbytes
+            line['gather_record'] = 'compact' if shard.compact else 'full'
             line['gather_mode'] = gather_mode
             line['gather_graph'] = gather_graph
         line['cpu_baseline'] = cpu
@@ -906,7 +910,7 @@ def nn_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
 
 METRIC_MNIST = ('vectorised env-steps/sec, Optimize-v0 at the reference default data shape '
                 '(mnist 7x7: 60000 x 49, 10 classes, B = N) @4096 envs, MI355X vs host CPU')
-MFMA_F64_PEAK_TFLOPS = 78.6    # MI355X spec, f64 matrix (measured 71: profiles/r02_mfma_f64.jsonl)
+MFMA_F64_PEAK_TFLOPS = 78.6    # MI355X spec, f64 matrix (16x16x4 f64 measured at ~32 ns per wave instruction: profiles/r03_mfma_valu_mix.jsonl)
 
 
 def mnist_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean):

@@ -15,7 +15,7 @@ if os.environ.get('CE_LIB') == 'diag':
 elif os.environ.get('CE_LIB'):
     LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd_%s.so' % os.environ['CE_LIB'])
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 CE_OK, CE_EINVAL, CE_EHIP, CE_ENOMEM, CE_ESTATE, CE_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
 CE_PROBLEM_SOFTMAX, CE_PROBLEM_MLP = 0, 1
 CE_F64, CE_F32 = 0, 1
@@ -55,7 +55,8 @@ class NativeEngineError(RuntimeError):
 class CeConfig(ctypes.Structure):
     _fields_ = [(name, ctypes.c_int32) for name in (
         'abi_version', 'problem', 'precision', 'device', 'num_envs', 'n_rows',
-        'n_features', 'n_classes', 'batch_size', 'max_steps', 'auto_reset', 'n_hidden')]
+        'n_features', 'n_classes', 'batch_size', 'max_steps', 'auto_reset', 'n_hidden',
+        'n_layers')] + [('hidden', ctypes.c_int32 * 4)]
 
 
 class CeOutputs(ctypes.Structure):

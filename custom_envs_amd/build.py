@@ -29,13 +29,14 @@ def _hipcc():
 
 def sources():
     return [os.path.join(CSRC, f) for f in ('engine.hip', 'optimize_mfma.hip', 'multi_engine.hip',
-                                            'multinn_engine.hip', 'seeding.cpp')]
+                                            'multinn_engine.hip', 'net_engine.hip', 'seeding.cpp')]
 
 
 def headers():
     return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'optimize_pair_kernel.h',
                                             'optimize_mfma_kernel.h', 'optimize_mfma.h', 'optimize_lr_mfma.h',
-                                            'multiopt_kernels.h', 'mlp_kernels.h', 'multinn_kernels.h', 'common.h', 'seeding.h')] + [
+                                            'multiopt_kernels.h', 'mlp_kernels.h', 'multinn_kernels.h', 'net_engine.h',
+                                            'common.h', 'seeding.h')] + [
         os.path.join(ROOT, 'include', 'custom_envs_amd.h')]
 
 
@@ -86,7 +87,9 @@ def _compile(out, tmp, defines, verbose):
     with ThreadPoolExecutor(max_workers=min(len(cmds), 8)) as pool:
         for proc in pool.map(lambda c: subprocess.run(c, check=True), cmds):
             pass
-    cmd = [hipcc, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out + '.tmp'] + objs
+    # rocBLAS: the layered network path's plain batched GEMMs (net_engine.hip)
+    cmd = [hipcc, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out + '.tmp'] + objs + [
+        '-L/opt/rocm/lib', '-lrocblas', '-Wl,-rpath,/opt/rocm/lib']
     subprocess.run(cmd, check=True)
     os.replace(out + '.tmp', out)
     return out

@@ -22,6 +22,7 @@
 
 #include "common.h"
 #include "mlp_kernels.h"
+#include "net_engine.h"
 #include "optimize_kernels.h"
 #include "optimize_mfma.h"
 #include "optimize_pair_kernel.h"
@@ -91,6 +92,8 @@ struct ce_engine {
     ce_config cfg{};
     int P = 0, obs_dim = 0;
     bool mlp = false;  // CE_PROBLEM_MLP
+    ce::NetPlan *net = nullptr;   // CE_PROBLEM_MLP on the layered path (net_engine.hip)
+    std::vector<int> dims;        // network: F, hidden..., K
     bool mlp_split = false;  // two launches per step (CE_MLP_SPLIT=1 or CE_MLP_PHASES)
     int mlp_phases = 3;  // bit 0: train kernel, bit 1: info kernel (CE_MLP_PHASES, profiling)
     size_t tsize = 8;  // element size of W / W0
@@ -221,8 +224,44 @@ ce::MlpArgs make_mlp_args(const ce_engine *e, const float *act, const ce_outputs
 
 // compact: the caller's device outputs are in the compact form
 // (ce_set_compact_outputs; only the two-class MFMA path writes it)
-void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &o,
-            hipStream_t stream, bool compact = false) {
+ce::NetArgs make_net_args(const ce_engine *e, const float *act, const ce_outputs &o) {
+    ce::NetArgs a{};
+    a.E = e->cfg.num_envs;
+    a.N = e->cfg.n_rows;
+    a.F = e->cfg.n_features;
+    a.K = e->cfg.n_classes;
+    a.B = e->cfg.batch_size;
+    a.P = e->P;
+    a.max_steps = e->cfg.max_steps;
+    a.auto_reset = e->cfg.auto_reset;
+    a.n_hidden = static_cast<int>(e->dims.size()) - 2;
+    for (int l = 0; l < a.n_hidden; ++l) a.hidden[l] = e->dims[l + 1];
+    a.X = static_cast<const float *>(e->X);
+    a.label = e->label;
+    a.W = static_cast<float *>(e->W);
+    a.W0 = static_cast<const float *>(e->W0);
+    a.G = static_cast<double *>(e->G);
+    a.L = e->L;
+    a.step = e->step;
+    a.perm = e->perm;
+    a.order = e->order;
+    a.order_sel = e->order_sel;
+    a.act = act;
+    a.obs = o.obs;
+    a.reward = o.reward;
+    a.done = o.done;
+    a.objective = o.objective;
+    a.accuracy = o.accuracy;
+    a.episode_len = o.episode_len;
+    return a;
+}
+
+int launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &o,
+           hipStream_t stream, bool compact = false) {
+    if (e->net) {
+        const ce::NetArgs a = make_net_args(e, act, o);
+        return reset ? ce::net_reset(e->net, a, stream) : ce::net_step(e->net, a, stream);
+    }
     if (e->mlp) {
         const ce::MlpArgs a = make_mlp_args(e, act, o);
         const dim3 grid(e->cfg.num_envs), block(ce::kMlpBlock);
@@ -242,7 +281,7 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
                 else hipLaunchKernelGGL(ce::mlp_info_kernel<false>, grid, block, 0, stream, a);
             }
         }
-        return;
+        return CE_OK;
     }
     if (e->lr_mfma) {
         auto a = make_args<double>(e, act, o, compact);
@@ -250,7 +289,7 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
             ce::gen_launch_reset(a, stream);
         else
             ce::lr_launch_step(a, stream);
-        return;
+        return CE_OK;
     }
     if (e->gen_ft) {
         auto a = make_args<double>(e, act, o);
@@ -258,7 +297,7 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
             ce::gen_launch_reset(a, stream);
         else
             ce::gen_launch_step(a, stream);
-        return;
+        return CE_OK;
     }
     StepFn fn = reset ? e->kern->reset
                       : (e->pair ? e->pair : (e->staged ? e->kern->step_staged : e->kern->step_global));
@@ -269,12 +308,17 @@ void launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &
         auto a = make_args<float>(e, act, o);
         fn(&a, grid_of(e), e->stage_bytes, stream);
     }
+    return CE_OK;
 }
 
 // k steps of every env, actions s * stride apart.
-void launch_steps(const ce_engine *e, int k, const float *actions, int64_t stride,
-                  const ce_outputs &o) {
-    for (int s = 0; s < k; ++s) launch(e, false, actions + s * stride, o, e->stream, e->compact);
+int launch_steps(const ce_engine *e, int k, const float *actions, int64_t stride,
+                 const ce_outputs &o) {
+    for (int s = 0; s < k; ++s) {
+        const int rc = launch(e, false, actions + s * stride, o, e->stream, e->compact);
+        if (rc != CE_OK) return rc;
+    }
+    return CE_OK;
 }
 
 // Convert host float64 values to a device array of `elem`-byte floats.
@@ -332,7 +376,8 @@ int do_step(ce_engine *e, const float *actions, const ce_outputs *out, uint32_t 
         if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
         ce_outputs o = out ? *out : region_view(e, e->d_out);
         if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
-        launch(e, false, actions, o, e->stream, e->compact);
+        const int rc = launch(e, false, actions, o, e->stream, e->compact);
+        if (rc != CE_OK) return rc;
         CE_HIP(hipGetLastError());
         if (sync) CE_HIP(hipStreamSynchronize(e->stream));
         return CE_OK;
@@ -340,7 +385,8 @@ int do_step(ce_engine *e, const float *actions, const ce_outputs *out, uint32_t 
     std::memcpy(e->h_act, actions, E * e->P * sizeof(float));
     CE_HIP(hipMemcpyAsync(e->d_act, e->h_act, E * e->P * sizeof(float), hipMemcpyHostToDevice,
                           e->stream));
-    launch(e, false, e->d_act, region_view(e, e->d_out), e->stream);
+    const int rc = launch(e, false, e->d_act, region_view(e, e->d_out), e->stream);
+    if (rc != CE_OK) return rc;
     CE_HIP(hipGetLastError());
     CE_HIP(hipMemcpyAsync(e->h_out, e->d_out, e->out_bytes, hipMemcpyDeviceToHost, e->stream));
     if (sync) {
@@ -392,16 +438,30 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     const bool mlp = cfg->problem == CE_PROBLEM_MLP;
     const KernelEntry *kern = nullptr;
     bool lr_path = false;
+    bool net_path = false;
+    std::vector<int> dims;
     if (mlp) {
-        // the shapes mlp_kernels.h is written for (config 3: 784 -> 64 -> 10, B = 32)
         if (cfg->precision != CE_F32)
             return fail(CE_EUNSUPPORTED, "ce_create: the MLP problem computes in float32");
-        if (cfg->n_hidden != ce::kMlpHidden || cfg->batch_size != ce::kMlpBatch ||
-            cfg->n_features % 8 != 0 || cfg->n_classes > ce::kMlpMaxK || cfg->n_rows % 64 != 0 ||
-            cfg->batch_size >= cfg->n_rows)
-            return fail(CE_EUNSUPPORTED, "ce_create: MLP needs n_hidden=64, batch_size=32 < "
-                                         "n_rows, n_rows % 64 == 0, n_features % 8 == 0, "
-                                         "n_classes <= 16");
+        if (cfg->n_layers < 0 || cfg->n_layers > ce::kNetMaxHidden)
+            return fail(CE_EUNSUPPORTED, "ce_create: the network takes 1 to 4 hidden layers");
+        dims.push_back(cfg->n_features);
+        if (cfg->n_layers == 0) dims.push_back(cfg->n_hidden);
+        for (int l = 0; l < cfg->n_layers; ++l) dims.push_back(cfg->hidden[l]);
+        dims.push_back(cfg->n_classes);
+        for (int d : dims)
+            if (d <= 0) return fail(CE_EINVAL, "ce_create: network widths must be positive");
+        // the fused config-3 kernel (mlp_kernels.h: 784 -> 64 -> 10, B = 32)
+        // where its shape holds; every other network on the layered path
+        // (net_engine.hip); CE_MLP_NET=1 forces the layered path (tests)
+        const char *fn = std::getenv("CE_MLP_NET");
+        const bool fused = !(fn && fn[0] == '1') && dims.size() == 3 &&
+                           dims[1] == ce::kMlpHidden && cfg->batch_size == ce::kMlpBatch &&
+                           cfg->n_features % 8 == 0 && cfg->n_classes <= ce::kMlpMaxK &&
+                           cfg->n_rows % 64 == 0 && cfg->batch_size < cfg->n_rows;
+        net_path = !fused;
+        if (net_path && cfg->n_classes > 32)
+            return fail(CE_EUNSUPPORTED, "ce_create: the network takes at most 32 classes");
     } else {
         // a register-path instance when the shape has one (unless CE_GENERIC=1
         // forces the runtime-shape kernel, for tests), else the MFMA kernel
@@ -438,6 +498,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     e->cfg = *cfg;
     e->kern = kern;
     e->mlp = mlp;
+    e->dims = dims;
     if (const char *md = std::getenv("CE_MANY_DIRECT")) e->many_direct = std::atoi(md);
     if (const char *lw = std::getenv("CE_LR_WAVES")) e->lr_waves = std::atoi(lw);
     if (const char *gt = std::getenv("CE_GEN_TAIL")) e->gen_tail = std::atoi(gt);
@@ -450,8 +511,13 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     }
     if (const char *sp = std::getenv("CE_MLP_SPLIT")) e->mlp_split = e->mlp_split || sp[0] == '1';
     if (mlp) {
-        const int F = cfg->n_features, H = cfg->n_hidden, K = cfg->n_classes;
-        e->P = F * H + H + H * K + K;
+        const int64_t P = ce::net_params(cfg->n_features, cfg->n_classes,
+                                         static_cast<int>(dims.size()) - 2, dims.data() + 1);
+        if (P > (int64_t(1) << 30)) {
+            delete e;
+            return fail(CE_EUNSUPPORTED, "ce_create: network too large (P > 2^30)");
+        }
+        e->P = static_cast<int>(P);
         e->tsize = sizeof(float);
         e->gsize = sizeof(double);
     } else {
@@ -479,7 +545,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     const size_t E = cfg->num_envs, N = cfg->n_rows, F = cfg->n_features, P = e->P;
     if (mlp) {
         CE_TRY(hipMalloc(&e->X, N * F * sizeof(float)));
-        CE_TRY(hipMalloc(&e->Xs, N * F * sizeof(float)));
+        if (!net_path) CE_TRY(hipMalloc(&e->Xs, N * F * sizeof(float)));
         CE_TRY(hipMalloc(&e->label, N * sizeof(int32_t)));
     } else if (lr_path) {
         e->lr_mfma = true;
@@ -534,16 +600,25 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         std::vector<float> x32(N * F);
         for (size_t i = 0; i < N * F; ++i) x32[i] = static_cast<float>(features[i]);
         CE_TRY(hipMemcpy(e->X, x32.data(), N * F * sizeof(float), hipMemcpyHostToDevice));
-        std::vector<float> xs(N * F);
-        const size_t chunks = F / 8;
-        for (size_t t = 0; t < N / 32; ++t)
-            for (size_t c = 0; c < chunks; ++c)
-                for (size_t l = 0; l < 64; ++l)
-                    for (size_t j = 0; j < 4; ++j)
-                        xs[((t * chunks + c) * 64 + l) * 4 + j] =
-                            x32[(32 * t + (l & 31)) * F + 8 * c + 4 * (l >> 5) + j];
-        CE_TRY(hipMemcpy(e->Xs, xs.data(), N * F * sizeof(float), hipMemcpyHostToDevice));
+        if (!net_path) {   // the fused kernel's operand-ordered copy
+            std::vector<float> xs(N * F);
+            const size_t chunks = F / 8;
+            for (size_t t = 0; t < N / 32; ++t)
+                for (size_t c = 0; c < chunks; ++c)
+                    for (size_t l = 0; l < 64; ++l)
+                        for (size_t j = 0; j < 4; ++j)
+                            xs[((t * chunks + c) * 64 + l) * 4 + j] =
+                                x32[(32 * t + (l & 31)) * F + 8 * c + 4 * (l >> 5) + j];
+            CE_TRY(hipMemcpy(e->Xs, xs.data(), N * F * sizeof(float), hipMemcpyHostToDevice));
+        }
         CE_TRY(hipMemcpy(e->label, labels, N * sizeof(int32_t), hipMemcpyHostToDevice));
+        if (net_path) {
+            const ce::NetArgs a = make_net_args(e, nullptr, region_view(e, e->d_out));
+            if ((rc = ce::net_create(&e->net, a, cfg->device)) != CE_OK) return bail(rc);
+            std::string name = "net<";
+            for (size_t i = 0; i < dims.size(); ++i) name += (i ? "," : "") + std::to_string(dims[i]);
+            e->kernel_name = name + ">";
+        }
     }
 #undef CE_TRY
     if (e->lr_mfma) {
@@ -630,6 +705,7 @@ void ce_destroy(ce_engine *e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     e->graphs.release();
+    ce::net_destroy(e->net);
     void *dev[] = {e->X, e->Xs, e->label, e->W, e->G, e->W0, e->L, e->step,
                    e->perm, e->order, e->order_sel, e->d_act, e->d_out, e->diag};
     for (void *p : dev)
@@ -668,22 +744,23 @@ int ce_seed(ce_engine *e, const uint64_t *seeds, int32_t n) {
     const bool with_perm = e->perm != nullptr;
     if (e->mlp) {
         std::vector<float> w0(E * P);
-        std::vector<int32_t> perm(E * N);
+        std::vector<int32_t> perm(with_perm ? E * N : 0);
         const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         const size_t nt = std::min<size_t>(hw, E);
         std::vector<std::thread> pool;
         for (size_t t = 0; t < nt; ++t)
             pool.emplace_back([&, t] {
                 for (size_t i = t; i < E; i += nt)
-                    ce::reset_draws_mlp(seeds[i], e->cfg.n_features, e->cfg.n_hidden,
-                                        e->cfg.n_classes, static_cast<int>(N), &w0[i * P],
-                                        &perm[i * N]);
+                    ce::reset_draws_net(seeds[i], static_cast<int>(e->dims.size()),
+                                        e->dims.data(), static_cast<int>(N), &w0[i * P],
+                                        with_perm ? &perm[i * N] : nullptr);
             });
         for (auto &th : pool) th.join();
         CE_HIP(hipMemcpyAsync(e->W0, w0.data(), E * P * sizeof(float), hipMemcpyHostToDevice,
                               e->stream));
-        CE_HIP(hipMemcpyAsync(e->perm, perm.data(), E * N * sizeof(int32_t),
-                              hipMemcpyHostToDevice, e->stream));
+        if (with_perm)
+            CE_HIP(hipMemcpyAsync(e->perm, perm.data(), E * N * sizeof(int32_t),
+                                  hipMemcpyHostToDevice, e->stream));
         CE_HIP(hipStreamSynchronize(e->stream));
         return CE_OK;
     }
@@ -707,12 +784,14 @@ int ce_reset(ce_engine *e, const ce_outputs *out, uint32_t flags) {
         if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
         if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
         ce_outputs o = out ? *out : region_view(e, e->d_out);
-        launch(e, true, nullptr, o, e->stream, e->compact);
+        const int rc = launch(e, true, nullptr, o, e->stream, e->compact);
+        if (rc != CE_OK) return rc;
         CE_HIP(hipGetLastError());
         e->was_reset = true;
         return CE_OK;
     }
-    launch(e, true, nullptr, region_view(e, e->d_out), e->stream);
+    const int rc = launch(e, true, nullptr, region_view(e, e->d_out), e->stream);
+    if (rc != CE_OK) return rc;
     CE_HIP(hipGetLastError());
     CE_HIP(hipMemcpyAsync(e->h_out, e->d_out, e->out_bytes, hipMemcpyDeviceToHost, e->stream));
     CE_HIP(hipStreamSynchronize(e->stream));
@@ -748,7 +827,7 @@ int many_graph(ce_engine *e, int32_t k, const float *actions, int64_t stride,
     if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
     const ce_outputs o = out ? *out : region_view(e, e->d_out);
     return e->graphs.get(ce::graph_key(k, 0, actions, stride, e->stream, o), [&] {
-        launch_steps(e, k, actions, stride, o);
+        (void)launch_steps(e, k, actions, stride, o);
     }, exec);
 }
 
@@ -762,7 +841,8 @@ int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
         if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
         if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
         const ce_outputs o = out ? *out : region_view(e, e->d_out);
-        launch_steps(e, k, actions, stride, o);
+        const int rc = launch_steps(e, k, actions, stride, o);
+        if (rc != CE_OK) return rc;
         CE_HIP(hipGetLastError());
         return CE_OK;
     }
@@ -781,7 +861,7 @@ int ce_step_many_prepare(ce_engine *e, int32_t k, const float *actions, int64_t 
 
 const char *ce_step_kernel(const ce_engine *e) {
     if (!e) return "";
-    if (e->mlp)
+    if (e->mlp && !e->net)
         return e->mlp_split ? "mlp_train_kernel+mlp_info_kernel"
                             : "mlp_step_kernel";
     return e->kernel_name.c_str();

@@ -1,0 +1,495 @@
+// Optimize-v0 over a general OptimizeNN network (net_engine.h has the step's
+// launch sequence).  The dense products of every layer are plain GEMMs over
+// the envs' parameter slabs -- strided-batched rocBLAS sgemm, batch = envs,
+// the dataset operand shared (stride 0) -- and everything around them is
+// hand-written: the update and the minibatch gather, bias + relu, the
+// softmax / cross-entropy / argmax with its per-env reductions, the bias
+// gradients, relu', and the float64 epilogue.
+#include "net_engine.h"
+
+#include <rocblas/rocblas.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "common.h"
+
+namespace ce {
+
+namespace {
+
+constexpr int kNetBlock = 256;
+constexpr int kNetMaxK = 32;
+
+template <typename T>
+int dev_alloc(T **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return CE_OK;
+    CE_HIP(hipMalloc(reinterpret_cast<void **>(p), count * sizeof(T)));
+    return CE_OK;
+}
+
+// W' = W - a over every env's parameters (optimize.py:74-75); the step
+// counter advances (baseenvironment.py:30-41: current_step += 1 first)
+__global__ __launch_bounds__(kNetBlock) void net_update_kernel(float *W, const float *act,
+                                                             size_t n, int32_t *step, int E) {
+    const size_t i0 = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kNetBlock;
+    for (size_t i = i0; i < n; i += stride) W[i] -= act[i];
+    if (i0 < static_cast<size_t>(E)) step[i0] += 1;
+}
+
+// sequence[0]: rows order[0 .. B) of each env's current order
+// (inmemorydataset.py:17-28 over the composed reset permutations)
+__global__ __launch_bounds__(kNetBlock) void net_gather_kernel(NetArgs a, float *xb, int32_t *yb) {
+    const int e = blockIdx.y;
+    const int sel = a.order_sel[e];
+    const int32_t *order = a.order + (static_cast<size_t>(sel) * a.E + e) * a.N;
+    const size_t n = static_cast<size_t>(a.B) * a.F;
+    float *dst = xb + static_cast<size_t>(e) * n;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; i < n;
+         i += static_cast<size_t>(gridDim.x) * kNetBlock) {
+        const int r = static_cast<int>(i / a.F), f = static_cast<int>(i - static_cast<size_t>(r) * a.F);
+        const int row = order[r];
+        dst[i] = a.X[static_cast<size_t>(row) * a.F + f];
+        if (f == 0) yb[static_cast<size_t>(e) * a.B + r] = a.label[row];
+    }
+}
+
+// H[e] (R x d) += b_l[e]; relu (the hidden Dense layers' activation)
+__global__ __launch_bounds__(kNetBlock) void net_bias_act_kernel(float *H, int R, int d,
+                                                               const float *W, int64_t P,
+                                                               int64_t offb) {
+    const int e = blockIdx.y;
+    const size_t n = static_cast<size_t>(R) * d;
+    float *h = H + static_cast<size_t>(e) * n;
+    const float *b = W + static_cast<size_t>(e) * P + offb;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; i < n;
+         i += static_cast<size_t>(gridDim.x) * kNetBlock) {
+        const int j = static_cast<int>(i % d);
+        h[i] = fmaxf(h[i] + b[j], 0.0f);
+    }
+}
+
+// One env per workgroup, rows strided over its threads: logits + b_out, the
+// row-max-stabilised softmax (utils_math.py:51-63), -log(p_y + 1e-16)
+// (utils_math.py:25-34), np.argmax's first maximum of P, and (when dz is
+// set) dZ = P - Y in place.  Per-env sums: the cross-entropy terms in
+// float64 and the hits.  Labels: y + e * y_stride (0: the shared labels).
+__global__ __launch_bounds__(kNetBlock) void net_softmax_kernel(float *Z, int R, int K,
+                                                              const float *W, int64_t P,
+                                                              int64_t offb, const int32_t *y,
+                                                              int64_t y_stride, bool dz,
+                                                              double *loss_out, int32_t *hits_out) {
+    __shared__ double sl[kNetBlock];
+    __shared__ int sh[kNetBlock];
+    const int e = blockIdx.x;
+    float *z = Z + static_cast<size_t>(e) * R * K;
+    const int32_t *ye = y + static_cast<size_t>(e) * y_stride;
+    const float *b = W + static_cast<size_t>(e) * P + offb;
+    float bk[kNetMaxK];
+#pragma unroll
+    for (int k = 0; k < kNetMaxK; ++k) bk[k] = k < K ? b[k] : 0.0f;
+    double loss = 0.0;
+    int hits = 0;
+    for (int r = threadIdx.x; r < R; r += kNetBlock) {
+        float *zr = z + static_cast<size_t>(r) * K;
+        float v[kNetMaxK];
+        float m = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < kNetMaxK; ++k) {
+            v[k] = k < K ? zr[k] + bk[k] : -INFINITY;
+            m = fmaxf(m, v[k]);
+        }
+        float s = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kNetMaxK; ++k) {
+            v[k] = k < K ? expf(v[k] - m) : 0.0f;
+            s += v[k];
+        }
+        const int yr = ye[r];
+        int arg = 0;
+        float best = -1.0f;
+#pragma unroll
+        for (int k = 0; k < kNetMaxK; ++k) {
+            if (k < K) {
+                v[k] = v[k] / s;                       // P
+                if (v[k] > best) {
+                    best = v[k];
+                    arg = k;
+                }
+            }
+        }
+        float py = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kNetMaxK; ++k) py = k == yr ? v[k] : py;
+        loss += static_cast<double>(-logf(py + 1e-16f));
+        hits += arg == yr ? 1 : 0;
+        if (dz) {
+#pragma unroll
+            for (int k = 0; k < kNetMaxK; ++k)
+                if (k < K) zr[k] = v[k] - (k == yr ? 1.0f : 0.0f);
+        }
+    }
+    sl[threadIdx.x] = loss;
+    sh[threadIdx.x] = hits;
+    __syncthreads();
+    for (int w = kNetBlock / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            sl[threadIdx.x] += sl[threadIdx.x + w];
+            sh[threadIdx.x] += sh[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        loss_out[e] = sl[0];
+        hits_out[e] = sh[0];
+    }
+}
+
+// db[e][j] = sum over rows of dZ[e][r][j], into the env's gradient slab
+__global__ __launch_bounds__(kNetBlock) void net_colsum_kernel(const float *dZ, int R, int d,
+                                                             float *grad, int64_t P, int64_t offb) {
+    const int e = blockIdx.y;
+    const int j = blockIdx.x * kNetBlock + threadIdx.x;
+    if (j >= d) return;
+    const float *z = dZ + static_cast<size_t>(e) * R * d + j;
+    float s = 0.0f;
+    for (int r = 0; r < R; ++r) s += z[static_cast<size_t>(r) * d];
+    grad[static_cast<size_t>(e) * P + offb + j] = s;
+}
+
+// dZ = dH * relu'(Z), relu'(Z) = (H > 0) on the post-relu activation
+__global__ __launch_bounds__(kNetBlock) void net_relu_back_kernel(float *dH, const float *H, size_t n) {
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; i < n;
+         i += static_cast<size_t>(gridDim.x) * kNetBlock)
+        if (!(H[i] > 0.0f)) dH[i] = 0.0f;
+}
+
+// Per (env, parameter): g = grad / B (float32, as numpy divides the float32
+// gradient), G' = g / (|G| + 1) in float64 (optimize.py:78-83, grad_hist
+// float64), obs = [0 (P) | L' (written per env) | G' (P)]; the auto-reset
+// (utils_venv.py:31) of an env whose step ends its episode: W <- W0, G <- 0,
+// obs <- 0 (the reset observation).  step[e] already holds current_step.
+__global__ __launch_bounds__(kNetBlock) void net_epilogue_kernel(NetArgs a, const float *grad) {
+    const int e = blockIdx.y;
+    const int cur = a.step[e];
+    const bool wipe = cur >= a.max_steps && a.auto_reset;
+    const size_t P = a.P, base = static_cast<size_t>(e) * P;
+    float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
+    const float fb = static_cast<float>(a.B);
+    for (size_t p = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; p < P;
+         p += static_cast<size_t>(gridDim.x) * kNetBlock) {
+        const float g = grad[base + p] / fb;
+        const double gn = static_cast<double>(g) / (fabs(a.G[base + p]) + 1.0);
+        obs[p] = 0.0f;                                    // wght_hist is identically 0
+        obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(gn);
+        a.G[base + p] = wipe ? 0.0 : gn;
+        if (wipe) a.W[base + p] = a.W0[base + p];
+    }
+}
+
+// Per env: L' = (loss - L)/(L + 0.1) (optimize.py:80-81), reward = -loss,
+// done = current_step >= max_steps (:102-103), info, episode length; the
+// auto-reset's L, step and order <- order[perm] (optimize.py:58-67).
+__global__ __launch_bounds__(kNetBlock) void net_finish_kernel(NetArgs a, const double *mb_loss,
+                                                             const int32_t *mb_hits,
+                                                             const double *inf_loss,
+                                                             const int32_t *inf_hits) {
+    const int e = blockIdx.x;
+    const int cur = a.step[e];
+    const bool done = cur >= a.max_steps;
+    const bool wipe = done && a.auto_reset;
+    __syncthreads();                                      // every thread has read step[e]
+    if (threadIdx.x == 0) {
+        // the loss is a float32 mean in the reference (TF / numpy float32)
+        const float loss = static_cast<float>(mb_loss[e] / a.B);
+        const float acc = static_cast<float>(static_cast<double>(mb_hits[e]) / a.B);
+        const bool full = a.B == a.N;
+        const float obj = full ? loss : static_cast<float>(inf_loss[e] / a.N);
+        const float oacc = full ? acc : static_cast<float>(static_cast<double>(inf_hits[e]) / a.N);
+        const double lprev = a.L[e];
+        const double lnew = (static_cast<double>(loss) - lprev) / (lprev + 0.1);
+        const size_t P = a.P;
+        a.obs[static_cast<size_t>(e) * (2 * P + 1) + P] = wipe ? 0.0f : static_cast<float>(lnew);
+        a.reward[e] = -loss;
+        a.done[e] = done ? 1 : 0;
+        a.objective[e] = obj;
+        a.accuracy[e] = oacc;
+        a.episode_len[e] = cur;
+        a.L[e] = wipe ? 0.0 : lnew;
+        a.step[e] = wipe ? 0 : cur;
+    }
+    if (wipe && a.order != nullptr) {
+        const int sel = a.order_sel[e];
+        const int32_t *cur_o = a.order + (static_cast<size_t>(sel) * a.E + e) * a.N;
+        int32_t *nxt = a.order + (static_cast<size_t>(1 - sel) * a.E + e) * a.N;
+        const int32_t *pm = a.perm + static_cast<size_t>(e) * a.N;
+        for (int i = threadIdx.x; i < a.N; i += kNetBlock) nxt[i] = cur_o[pm[i]];
+        __syncthreads();
+        if (threadIdx.x == 0) a.order_sel[e] = 1 - sel;
+    }
+}
+
+// Reset (optimize.py:58-67): W <- W0, G <- 0, obs <- 0, then per env L,
+// step and order <- order[perm]
+__global__ __launch_bounds__(kNetBlock) void net_reset_params_kernel(NetArgs a) {
+    const int e = blockIdx.y;
+    const size_t P = a.P, base = static_cast<size_t>(e) * P;
+    float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
+    for (size_t p = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; p < 2 * P + 1;
+         p += static_cast<size_t>(gridDim.x) * kNetBlock) {
+        obs[p] = 0.0f;
+        if (p < P) {
+            a.W[base + p] = a.W0[base + p];
+            a.G[base + p] = 0.0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kNetBlock) void net_reset_env_kernel(NetArgs a) {
+    const int e = blockIdx.x;
+    if (threadIdx.x == 0) {
+        a.L[e] = 0.0;
+        a.step[e] = 0;
+    }
+    if (a.order != nullptr) {
+        const int sel = a.order_sel[e];
+        const int32_t *cur_o = a.order + (static_cast<size_t>(sel) * a.E + e) * a.N;
+        int32_t *nxt = a.order + (static_cast<size_t>(1 - sel) * a.E + e) * a.N;
+        const int32_t *pm = a.perm + static_cast<size_t>(e) * a.N;
+        for (int i = threadIdx.x; i < a.N; i += kNetBlock) nxt[i] = cur_o[pm[i]];
+        __syncthreads();
+        if (threadIdx.x == 0) a.order_sel[e] = 1 - sel;
+    }
+}
+
+unsigned blocks_for(size_t n, unsigned cap) {
+    const size_t b = (n + kNetBlock - 1) / kNetBlock;
+    return static_cast<unsigned>(std::max<size_t>(1, std::min<size_t>(b, cap)));
+}
+
+}  // namespace
+
+struct NetPlan {
+    rocblas_handle blas = nullptr;
+    void *workspace = nullptr;
+    int nl = 0;                             // dense layers (hidden + output)
+    int dims[kNetMaxHidden + 2] = {0};      // F, hidden..., K
+    int64_t offW[kNetMaxHidden + 1] = {0}, offb[kNetMaxHidden + 1] = {0};
+    int dmax = 0;
+    float *xb = nullptr;                    // [E][B][F] gathered minibatch rows (B < N)
+    int32_t *yb = nullptr;                  // [E][B]
+    float *mb_act[kNetMaxHidden] = {nullptr};   // [E][B][d_l] hidden activations (post-relu)
+    float *mb_out = nullptr;                // [E][B][K] logits, then dZ
+    float *dbuf[2] = {nullptr, nullptr};    // [E][B][dmax] dH / dZ ping-pong
+    float *grad = nullptr;                  // [E][P] summed gradient (float32)
+    float *inf[2] = {nullptr, nullptr};     // [E][N][dmax] info activations (B < N)
+    float *inf_out = nullptr;               // [E][N][K]
+    double *mb_loss = nullptr, *inf_loss = nullptr;
+    int32_t *mb_hits = nullptr, *inf_hits = nullptr;
+};
+
+int64_t net_params(int F, int K, int n_hidden, const int *hidden) {
+    int64_t P = 0;
+    int prev = F;
+    for (int l = 0; l <= n_hidden; ++l) {
+        const int d = l < n_hidden ? hidden[l] : K;
+        P += static_cast<int64_t>(prev) * d + d;
+        prev = d;
+    }
+    return P;
+}
+
+namespace {
+
+// Row-major C[M][N] (row stride ldc) = op(A) op(B), op(A) M x K, op(B) K x N,
+// batched over envs with element strides (0: shared operand).  rocBLAS is
+// column-major: a row-major matrix is its column-major transpose, so the
+// call computes C^T = op(B)^T op(A)^T with the operands swapped.
+int gemm_rm(rocblas_handle h, bool tA, bool tB, int M, int N, int K, const float *A, int lda,
+            int64_t sA, const float *B, int ldb, int64_t sB, float *C, int ldc, int64_t sC,
+            int batch) {
+    const float one = 1.0f, zero = 0.0f;
+    const rocblas_status st = rocblas_sgemm_strided_batched(
+        h, tB ? rocblas_operation_transpose : rocblas_operation_none,
+        tA ? rocblas_operation_transpose : rocblas_operation_none, N, M, K, &one, B, ldb, sB, A,
+        lda, sA, &zero, C, ldc, sC, batch);
+    if (st != rocblas_status_success)
+        return fail(CE_EHIP, std::string("rocblas_sgemm_strided_batched failed: ") +
+                                 rocblas_status_to_string(st));
+    return CE_OK;
+}
+
+}  // namespace
+
+int net_create(NetPlan **out, const NetArgs &a, int device) {
+    *out = nullptr;
+    if (a.n_hidden < 1 || a.n_hidden > kNetMaxHidden)
+        return fail(CE_EUNSUPPORTED, "network: 1 to 4 hidden layers");
+    if (a.K > kNetMaxK) return fail(CE_EUNSUPPORTED, "network: at most 32 classes");
+    if (a.E > 65535) return fail(CE_EUNSUPPORTED, "network: at most 65535 envs per engine");
+    NetPlan *p = new (std::nothrow) NetPlan();
+    if (!p) return fail(CE_ENOMEM, "network: host allocation failed");
+    auto bail = [&](int rc) {
+        net_destroy(p);
+        return rc;
+    };
+    p->nl = a.n_hidden + 1;
+    p->dims[0] = a.F;
+    for (int l = 0; l < a.n_hidden; ++l) {
+        if (a.hidden[l] <= 0) return bail(fail(CE_EINVAL, "network: hidden widths must be positive"));
+        p->dims[l + 1] = a.hidden[l];
+    }
+    p->dims[p->nl] = a.K;
+    int64_t off = 0;
+    for (int l = 0; l < p->nl; ++l) {
+        p->offW[l] = off;
+        off += static_cast<int64_t>(p->dims[l]) * p->dims[l + 1];
+        p->offb[l] = off;
+        off += p->dims[l + 1];
+        if (l < a.n_hidden) p->dmax = std::max(p->dmax, p->dims[l + 1]);
+    }
+    if (off != a.P) return bail(fail(CE_EINVAL, "network: parameter count mismatch"));
+    const size_t E = a.E, B = a.B, N = a.N;
+    int rc;
+    if (hipSetDevice(device) != hipSuccess) return bail(fail(CE_EHIP, "network: hipSetDevice"));
+    if (B < N) {
+        if ((rc = dev_alloc(&p->xb, E * B * a.F)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->yb, E * B)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->inf[0], E * N * p->dmax)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->inf[1], E * N * p->dmax)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->inf_out, E * N * a.K)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->inf_loss, E)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->inf_hits, E)) != CE_OK) return bail(rc);
+    }
+    for (int l = 0; l < a.n_hidden; ++l)
+        if ((rc = dev_alloc(&p->mb_act[l], E * B * p->dims[l + 1])) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->mb_out, E * B * a.K)) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->dbuf[0], E * B * p->dmax)) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->dbuf[1], E * B * p->dmax)) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->grad, E * static_cast<size_t>(a.P))) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->mb_loss, E)) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->mb_hits, E)) != CE_OK) return bail(rc);
+    if (rocblas_create_handle(&p->blas) != rocblas_status_success)
+        return bail(fail(CE_EHIP, "network: rocblas_create_handle failed"));
+    // a fixed workspace, so no call allocates (hipGraph capture, ce_step_many)
+    constexpr size_t kWorkspace = 64u << 20;
+    if (hipMalloc(&p->workspace, kWorkspace) != hipSuccess)
+        return bail(fail(CE_ENOMEM, "network: workspace allocation failed"));
+    if (rocblas_set_workspace(p->blas, p->workspace, kWorkspace) != rocblas_status_success)
+        return bail(fail(CE_EHIP, "network: rocblas_set_workspace failed"));
+    *out = p;
+    return CE_OK;
+}
+
+void net_destroy(NetPlan *p) {
+    if (!p) return;
+    if (p->blas) rocblas_destroy_handle(p->blas);
+    void *bufs[] = {p->workspace, p->xb, p->yb, p->mb_out, p->dbuf[0], p->dbuf[1], p->grad,
+                    p->inf[0], p->inf[1], p->inf_out, p->mb_loss, p->inf_loss, p->mb_hits,
+                    p->inf_hits};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    for (float *b : p->mb_act)
+        if (b) (void)hipFree(b);
+    delete p;
+}
+
+int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
+    const int E = a.E, B = a.B, N = a.N, K = a.K, nl = p->nl;
+    const int64_t P = a.P;
+    const bool full = B == N;
+    if (rocblas_set_stream(p->blas, s) != rocblas_status_success)
+        return fail(CE_EHIP, "network: rocblas_set_stream failed");
+    const size_t EP = static_cast<size_t>(E) * P;
+    hipLaunchKernelGGL(net_update_kernel, dim3(blocks_for(EP, 8192)), dim3(kNetBlock), 0, s, a.W,
+                       a.act, EP, a.step, E);
+    // the minibatch: gathered rows (B < N) or the shared dataset (B == N)
+    const float *x = full ? a.X : p->xb;
+    const int64_t sx = full ? 0 : static_cast<int64_t>(B) * a.F;
+    const int32_t *y = full ? a.label : p->yb;
+    const int64_t sy = full ? 0 : B;
+    if (!full)
+        hipLaunchKernelGGL(net_gather_kernel, dim3(blocks_for(static_cast<size_t>(B) * a.F, 64), E),
+                           dim3(kNetBlock), 0, s, a, p->xb, p->yb);
+    int rc;
+    // forward on the minibatch
+    const float *h = x;
+    int64_t sh = sx;
+    for (int l = 0; l < nl; ++l) {
+        const int din = p->dims[l], dout = p->dims[l + 1];
+        float *o = l + 1 < nl ? p->mb_act[l] : p->mb_out;
+        if ((rc = gemm_rm(p->blas, false, false, B, dout, din, h, din, sh, a.W + p->offW[l], dout, P,
+                          o, dout, static_cast<int64_t>(B) * dout, E)) != CE_OK)
+            return rc;
+        if (l + 1 < nl)
+            hipLaunchKernelGGL(net_bias_act_kernel,
+                               dim3(blocks_for(static_cast<size_t>(B) * dout, 64), E),
+                               dim3(kNetBlock), 0, s, o, B, dout, a.W, P, p->offb[l]);
+        h = o;
+        sh = static_cast<int64_t>(B) * dout;
+    }
+    hipLaunchKernelGGL(net_softmax_kernel, dim3(E), dim3(kNetBlock), 0, s, p->mb_out, B, K, a.W, P,
+                       p->offb[nl - 1], y, sy, true, p->mb_loss, p->mb_hits);
+    // backward: dW_l = H_{l-1}^T dZ_l, db_l, dH_{l-1} = dZ_l W_l^T, relu'
+    const float *dz = p->mb_out;
+    for (int l = nl - 1; l >= 0; --l) {
+        const int din = p->dims[l], dout = p->dims[l + 1];
+        const float *hin = l == 0 ? x : p->mb_act[l - 1];
+        const int64_t shin = l == 0 ? sx : static_cast<int64_t>(B) * din;
+        const int64_t sdz = static_cast<int64_t>(B) * dout;
+        if ((rc = gemm_rm(p->blas, true, false, din, dout, B, hin, din, shin, dz, dout, sdz,
+                          p->grad + p->offW[l], dout, P, E)) != CE_OK)
+            return rc;
+        hipLaunchKernelGGL(net_colsum_kernel, dim3((dout + kNetBlock - 1) / kNetBlock, E),
+                           dim3(kNetBlock), 0, s, dz, B, dout, p->grad, P, p->offb[l]);
+        if (l == 0) break;
+        float *dh = p->dbuf[l & 1];
+        if ((rc = gemm_rm(p->blas, false, true, B, din, dout, dz, dout, sdz, a.W + p->offW[l], dout,
+                          P, dh, din, static_cast<int64_t>(B) * din, E)) != CE_OK)
+            return rc;
+        const size_t n = static_cast<size_t>(E) * B * din;
+        hipLaunchKernelGGL(net_relu_back_kernel, dim3(blocks_for(n, 8192)), dim3(kNetBlock), 0, s,
+                           dh, p->mb_act[l - 1], n);
+        dz = dh;
+    }
+    // info['objective'] / ['accuracy'] on every row (B < N)
+    if (!full) {
+        const float *hi = a.X;
+        int64_t shi = 0;
+        for (int l = 0; l < nl; ++l) {
+            const int din = p->dims[l], dout = p->dims[l + 1];
+            float *o = l + 1 < nl ? p->inf[l & 1] : p->inf_out;
+            if ((rc = gemm_rm(p->blas, false, false, N, dout, din, hi, din, shi, a.W + p->offW[l],
+                              dout, P, o, dout, static_cast<int64_t>(N) * dout, E)) != CE_OK)
+                return rc;
+            if (l + 1 < nl)
+                hipLaunchKernelGGL(net_bias_act_kernel,
+                                   dim3(blocks_for(static_cast<size_t>(N) * dout, 256), E),
+                                   dim3(kNetBlock), 0, s, o, N, dout, a.W, P, p->offb[l]);
+            hi = o;
+            shi = static_cast<int64_t>(N) * dout;
+        }
+        hipLaunchKernelGGL(net_softmax_kernel, dim3(E), dim3(kNetBlock), 0, s, p->inf_out, N, K, a.W,
+                           P, p->offb[nl - 1], a.label, int64_t(0), false, p->inf_loss, p->inf_hits);
+    }
+    hipLaunchKernelGGL(net_epilogue_kernel, dim3(blocks_for(static_cast<size_t>(P), 1024), E),
+                       dim3(kNetBlock), 0, s, a, p->grad);
+    hipLaunchKernelGGL(net_finish_kernel, dim3(E), dim3(kNetBlock), 0, s, a, p->mb_loss, p->mb_hits,
+                       p->inf_loss, p->inf_hits);
+    CE_HIP(hipGetLastError());
+    return CE_OK;
+}
+
+int net_reset(NetPlan *p, const NetArgs &a, hipStream_t s) {
+    (void)p;
+    hipLaunchKernelGGL(net_reset_params_kernel,
+                       dim3(blocks_for(2 * static_cast<size_t>(a.P) + 1, 1024), a.E), dim3(kNetBlock),
+                       0, s, a);
+    hipLaunchKernelGGL(net_reset_env_kernel, dim3(a.E), dim3(kNetBlock), 0, s, a);
+    CE_HIP(hipGetLastError());
+    return CE_OK;
+}
+
+}  // namespace ce

@@ -35,11 +35,32 @@
 // matrix rate equals the f64 vector rate on gfx950), ~0.7 us epilogue.
 #pragma once
 
+#include <type_traits>
+
 #include "optimize_kernels.h"
 
 namespace ce {
 
 typedef double lr_d4 __attribute__((ext_vector_type(4)));
+
+// Round-3 levers (each a build switch for A/B runs; the defaults are the
+// measured winners):
+//  CE_LR_W0_LAZY  the reset weights W0 are loaded only for envs whose step
+//                 wipes (1 step in 40), after the step counter has arrived
+//  CE_LR_RCP1     1/(1 + t) from v_rcp_f64 plus ONE Newton step (<= 11 ulp,
+//                 profiles/r01_rcp_accuracy.json) instead of two
+//  CE_LR_NOCLAMP  a workgroup whose |u| bound (sum_f |w'_f0 - w'_f1| max_r
+//                 |x_rf|, host-computed column maxima) stays below 650 runs
+//                 the row loop without the exp argument clamp
+#ifndef CE_LR_W0_LAZY
+#define CE_LR_W0_LAZY 1
+#endif
+#ifndef CE_LR_RCP1
+#define CE_LR_RCP1 1
+#endif
+#ifndef CE_LR_NOCLAMP
+#define CE_LR_NOCLAMP 1
+#endif
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
 constexpr int kLrMaxF = 16;
@@ -63,7 +84,9 @@ __host__ __device__ constexpr int lr_tile_doubles(int nkf) { return (nkf + 4 + 2
 //   [nkf + q]  gradient A X~[16t + (l>>4) + 4q][l&15]             q < 4
 //   [nkf + 4]  int32 pair: labels of rows 16t + (l>>4) + 4q, q = 0, 1
 //   [nkf + 5]  int32 pair: q = 2, 3
-// (layout [tile][slot][lane]; built by the engine at ce_create)
+// (layout [tile][slot][lane]; built by the engine at ce_create), then
+// kLrMaxF doubles: max over rows of |x[r][f]| (0 past F), the column maxima
+// of the |u| bound (CE_LR_NOCLAMP)
 
 // MODE (lr_mode): 0 = one tile at a time, padding rows (label -1) masked
 // out of every statistic; 1 = N a multiple of 16 and every wave owning the
@@ -88,6 +111,14 @@ __device__ __forceinline__ double clamp_u(double u) {
     asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(u), "v"(-700.0));
     asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(r), "v"(750.0));
     return r;
+}
+
+// 1/d for d in [1, 2^1010]: hardware reciprocal (~2^-24) + one Newton step,
+// within 11 ulp (profiles/r01_rcp_accuracy.json); p_y and q feed sums whose
+// float32 outputs are compared at 1e-6
+__device__ __forceinline__ double rcp_newton1(double d) {
+    const double r = __builtin_amdgcn_rcp(d);
+    return fma(r, fma(-d, r, 1.0), r);
 }
 
 // 1/d for any normal finite d != 0: hardware reciprocal + two Newton steps
@@ -190,12 +221,19 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     //    and the step counter.
     double2 wv[NKF];
     float2 av[NKF];
+#if CE_LR_NOCLAMP
+    double xm[NKF];                                     // max_r |x[r][4k + h]|
+    const double *colmax = img + static_cast<unsigned>(ntiles) * TD;
+#endif
 #pragma unroll
     for (int k = 0; k < NKF; ++k) {
         const int f = 4 * k + h;
         const unsigned i0 = pbase + (f < F ? 2 * f : 0);
         wv[k] = *reinterpret_cast<const double2 *>(a.W + i0);   // 16-B aligned: P even
         av[k] = *reinterpret_cast<const float2 *>(a.act + i0);  // 8-B aligned
+#if CE_LR_NOCLAMP
+        xm[k] = colmax[f];
+#endif
     }
     const int np_ = kLrEnvs * P;
     int pj[PR], pp[PR], step_p[PR];
@@ -210,7 +248,11 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
         prole[r] = i < np_ && e0 + pj[r] < a.E;
         gi[r] = static_cast<unsigned>(prole[r] ? e0 + pj[r] : 0) * P + (prole[r] ? pp[r] : 0);
         g_prev[r] = a.G[gi[r]];
+#if CE_LR_W0_LAZY
+        w_init[r] = 0.0;                                // loaded below, wiping envs only
+#else
         w_init[r] = a.W0[gi[r]];
+#endif
         step_p[r] = a.step[prole[r] ? e0 + pj[r] : 0];
     }
     const int sj = tid - (kLrBlock - kLrEnvs);
@@ -261,6 +303,21 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
             wsh[c][2 * f + 1] = w1;
         }
     }
+#if CE_LR_NOCLAMP
+    // |u| <= sum_f |x_f| |w'_f0 - w'_f1| <= sum_f max_r |x_rf| |wd_f| (the
+    // rounding of u and of this sum is ~1e-15 relative): below 650, no u can
+    // leave the exp's [-700, 750] argument range, so the row loop runs
+    // without the clamp.  Every wave forms the same wd, so the choice is
+    // uniform over the workgroup.
+    double ub = 0.0;
+#pragma unroll
+    for (int k = 0; k < NKF; ++k) ub = fma(fabs(wd[k]), xm[k], ub);
+    ub = fold_pair<16>(ub, ub);
+    ub = fold_pair<32>(ub, ub);
+    const bool bounded = __all(ub < 650.0);
+#else
+    const bool bounded = false;
+#endif
     const int cur = step_prev + 1;
     // the epilogue's divisors are known now: their reciprocals leave the
     // critical path (div_rcp)
@@ -275,9 +332,20 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
         // epilogue would wait for the completion of every store issued
         // before it; and left alone the compiler sinks the reciprocals into
         // the epilogue.
+#if CE_LR_W0_LAZY
+        asm volatile("" : "+v"(rG[r]) : "v"(step_p[r]));
+#else
         asm volatile("" : "+v"(rG[r]) : "v"(w_init[r]), "v"(step_p[r]));
+#endif
     }
     asm volatile("" : "+v"(rB), "+v"(rL));
+#if CE_LR_W0_LAZY
+    // W0 only where this step wipes (the auto-reset, utils_venv.py:31): one
+    // step in 40; the load runs under the row work and is pinned after it
+#pragma unroll
+    for (int r = 0; r < PR; ++r)
+        if (prole[r] && step_p[r] + 1 >= a.max_steps && a.auto_reset) w_init[r] = a.W0[gi[r]];
+#endif
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -300,18 +368,25 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     // chains cover the f64 latency), 2 at 4 waves per SIMD (the other waves
     // cover it, and the 128-register budget has no room for 4)
     constexpr int QC = W >= 16 ? 2 : 4;
-    auto softmax = [&](const lr_d4 &u, const int (&ys)[4], double (&qv)[4]) {
+    auto softmax = [&](auto clamp_c, const lr_d4 &u, const int (&ys)[4], double (&qv)[4]) {
 #pragma unroll
         for (int q0 = 0; q0 < 4; q0 += QC) {
             double tx[QC];
 #pragma unroll
-            for (int i = 0; i < QC; ++i) tx[i] = clamp_u(u[q0 + i]);
+            for (int i = 0; i < QC; ++i) {
+                if constexpr (decltype(clamp_c)::value) tx[i] = clamp_u(u[q0 + i]);
+                else tx[i] = u[q0 + i];
+            }
             exp_neg_q<QC>(tx);                          // t = e^-u
 #pragma unroll
             for (int i = 0; i < QC; ++i) {
                 const int q = q0 + i;
                 const double uq = u[q];
+#if CE_LR_RCP1
+                const double inv = rcp_newton1(1.0 + tx[i]);   // p_y
+#else
                 const double inv = rcp_unit(1.0 + tx[i]);   // p_y
+#endif
                 const bool valid = !PAD || ys[q] >= 0;
                 qv[q] = valid ? tx[i] * inv : 0.0;
                 prod *= valid ? inv + 1e-16 : 1.0;
@@ -358,6 +433,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     const int t_first = wave;
 #endif
     const int none[4] = {0, 0, 0, 0};
+    auto row_loop = [&](auto clamp_c) {
     for (int t = t_first; t < ntiles; t += NT * kLrWaves) {
         since += NT;
         if (since > 4) {                                // 16 factors in (1e-16, 1]: fold
@@ -389,10 +465,13 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             double qv[4];
-            softmax(u[i], PAD ? ys[i] : none, qv);
+            softmax(clamp_c, u[i], PAD ? ys[i] : none, qv);
             gradient(i, qv);
         }
     }
+    };
+    if (bounded) row_loop(std::false_type{});
+    else row_loop(std::true_type{});
     // a tie (p0 == p1) is np.argmax's class 0: hit iff y == 0.  Only a wave
     // that saw |u| < 2^-52 re-walks its tiles with the exact test e^-|u| == 1
     // (practically never).
@@ -411,6 +490,10 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
                 if (yv[q] >= 0 && tx[q] == 1.0) hits += (yv[q] == 0 ? 1 : 0) - (uu[q] > 0.0 ? 1 : 0);
         }
     }
+#if CE_LR_W0_LAZY
+#pragma unroll
+    for (int r = 0; r < PR; ++r) asm volatile("" : "+v"(w_init[r]));
+#endif
     // outputs nothing reads back in this launch, issued once the row loop
     // has consumed its loads (vmcnt counts stores as well): the
     // observation's weight part (wght_hist is identically 0), done and the

@@ -7,6 +7,7 @@
 #include "optimize_mfma_kernel.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 
@@ -106,7 +107,7 @@ constexpr GenFn kLrSteps[4] = {launch_lr<1>, launch_lr<2>, launch_lr<3>, launch_
 bool lr_shape_ok(int n_features, int n_classes) { return lr_mfma_shape(n_features, n_classes); }
 
 size_t lr_image_doubles(int n_features, int n_rows) {
-    return static_cast<size_t>((n_rows + 15) / 16) * lr_tile_doubles(lr_nkf(n_features));
+    return static_cast<size_t>((n_rows + 15) / 16) * lr_tile_doubles(lr_nkf(n_features)) + kLrMaxF;
 }
 
 void lr_build_image(int F, int N, const double *x, const int32_t *y, double *img) {
@@ -128,6 +129,12 @@ void lr_build_image(int F, int N, const double *x, const int32_t *y, double *img
             std::memcpy(&ti[(nkf + 4) * kWave + l], &lab[0], 8);
             std::memcpy(&ti[(nkf + 5) * kWave + l], &lab[2], 8);
         }
+    }
+    double *colmax = img + static_cast<size_t>(ntiles) * TD;   // the |u| bound's column maxima
+    for (int f = 0; f < kLrMaxF; ++f) {
+        double m = 0.0;
+        for (int r = 0; f < F && r < N; ++r) m = std::max(m, std::fabs(x[static_cast<size_t>(r) * F + f]));
+        colmax[f] = m;
     }
 }
 

@@ -235,29 +235,37 @@ static void legacy_shuffle(Mt19937 &rng, int n_rows, int32_t *perm) {
     }
 }
 
-void reset_draws_mlp(uint64_t seed, int n_features, int n_hidden, int n_classes, int n_rows,
-                     float *init_weights, int32_t *perm) {
+void reset_draws_net(uint64_t seed, int n_dims, const int *dims, int n_rows, float *init_weights,
+                     int32_t *perm) {
     uint32_t key[2];
     const int key_len = seed_key(seed, key);
     Mt19937 rng;
     rng.init_by_array(key, key_len);
-    // RandomState.uniform(low, high): low + (high - low) * random_sample()
-    auto draw = [&](int fan_in, int fan_out, float *out, int count) {
+    // RandomState.uniform(low, high): low + (high - low) * random_sample(),
+    // layer by layer in trainable_variables order, biases zero
+    size_t off = 0;
+    for (int l = 0; l + 1 < n_dims; ++l) {
+        const int fan_in = dims[l], fan_out = dims[l + 1];
         const double limit = std::sqrt(6.0 / static_cast<double>(fan_in + fan_out));
         const double low = -limit, range = limit - low;
-        for (int i = 0; i < count; ++i) {
+        const size_t n = static_cast<size_t>(fan_in) * fan_out;
+        for (size_t i = 0; i < n; ++i) {
             const double v = low + range * rng.next_double();
-            if (out) out[i] = static_cast<float>(v);
+            if (init_weights) init_weights[off + i] = static_cast<float>(v);
         }
-    };
-    const int w1 = n_features * n_hidden, w2 = n_hidden * n_classes;
-    draw(n_features, n_hidden, init_weights, w1);
-    draw(n_hidden, n_classes, init_weights ? init_weights + w1 + n_hidden : nullptr, w2);
-    if (init_weights) {
-        for (int i = 0; i < n_hidden; ++i) init_weights[w1 + i] = 0.0f;
-        for (int i = 0; i < n_classes; ++i) init_weights[w1 + n_hidden + w2 + i] = 0.0f;
+        off += n;
+        if (init_weights)
+            for (int i = 0; i < fan_out; ++i) init_weights[off + i] = 0.0f;
+        off += fan_out;
     }
+    // then sequence.shuffle() on the same stream (optimize.py:63-64)
     if (perm) legacy_shuffle(rng, n_rows, perm);
+}
+
+void reset_draws_mlp(uint64_t seed, int n_features, int n_hidden, int n_classes, int n_rows,
+                     float *init_weights, int32_t *perm) {
+    const int dims[3] = {n_features, n_hidden, n_classes};
+    reset_draws_net(seed, 3, dims, n_rows, init_weights, perm);
 }
 
 }  // namespace ce

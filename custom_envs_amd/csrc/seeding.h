@@ -35,6 +35,10 @@ void reset_draws(uint64_t seed, int n_features, int n_classes, int n_rows,
 // shuffle of arange(n_rows).  Either output may be null.
 void reset_draws_mlp(uint64_t seed, int n_features, int n_hidden, int n_classes, int n_rows,
                      float *init_weights, int32_t *perm);
+// The same for any depth (dims = F, hidden..., K): every layer's kernel
+// glorot-uniform in order, zero biases, then the shuffle on the same stream.
+void reset_draws_net(uint64_t seed, int n_dims, const int *dims, int n_rows, float *init_weights,
+                     int32_t *perm);
 
 // MultiOptLRs over the OptimizeNN problem (oracle/multinn.py nn_draws):
 // glorot-uniform kernels of every layer (dims[0] -> dims[1] -> ...) as legacy

@@ -65,8 +65,9 @@ class OptimizeEngine:
     def __init__(self, features, targets, num_envs, batch_size=None, max_steps=40,
                  precision=None, device=0, auto_reset=True, model='linear', hidden=64):
         """``model``: 'linear' (the build-defined ModelNumpy softmax classifier,
-        float64 by default) or 'mlp' (config 3: F -> hidden relu -> K softmax,
-        float32)."""
+        float64 by default) or 'mlp' (the OptimizeNN network: F -> hidden...
+        relu -> K softmax, float32; ``hidden`` a width or up to 4
+        widths; hidden=64 with batch_size=32 is config 3's fused kernel)."""
         if model not in MODELS:
             raise ValueError('model must be one of %s' % sorted(MODELS))
         if precision is None:
@@ -82,14 +83,23 @@ class OptimizeEngine:
         self.batch_size = n_rows if batch_size is None else int(batch_size)
         self.max_steps = int(max_steps)
         self.precision = precision
-        self.model, self.hidden = model, int(hidden)
+        # hidden: one width (config 3: 64) or a tuple of widths, e.g. the
+        # reference's create_neural_net default (256, 256)
+        self.model = model
+        self.hidden = int(hidden) if np.isscalar(hidden) else tuple(int(h) for h in hidden)
         self.device = int(device)
+        layers = (self.hidden,) if isinstance(self.hidden, int) else self.hidden
+        if model == 'mlp' and not 1 <= len(layers) <= 4:
+            raise ValueError('hidden: 1 to 4 layer widths')
         cfg = CeConfig(abi_version=_native.ABI_VERSION, problem=MODELS[model],
                        precision=PRECISIONS[precision], device=self.device,
                        num_envs=self.num_envs, n_rows=n_rows, n_features=n_features,
                        n_classes=n_classes, batch_size=self.batch_size,
                        max_steps=self.max_steps, auto_reset=1 if auto_reset else 0,
-                       n_hidden=self.hidden if model == 'mlp' else 0)
+                       n_hidden=layers[0] if model == 'mlp' else 0,
+                       n_layers=len(layers) if model == 'mlp' and len(layers) > 1 else 0)
+        for i, width in enumerate(layers if model == 'mlp' else ()):
+            cfg.hidden[i] = width
         self._labels = np.ascontiguousarray(labels, dtype=np.int32)
         handle = ctypes.c_void_p()
         check(lib.ce_create(ctypes.byref(cfg), features.ctypes.data, self._labels.ctypes.data,

@@ -260,7 +260,8 @@ class NNMultiEngine(MultiOptEngine):
         if arr.size != self.num_envs:
             raise ValueError('one seed per env')
         self._call('seed', arr.ctypes.data, int(arr.size))
-        return list(seeds)
+        self.seeds = [int(v) for v in arr]       # the current per-env seeds
+        return list(self.seeds)
 
     def get_state(self):
         E, P, N = self.num_envs, self.n_params, self.n_rows

@@ -116,10 +116,20 @@ class VecMonitor:
     ``file_paths`` is one path (or None) per env, as the per-env Monitors of
     the reference had; ``step`` takes per-env rewards, dones and an info
     sequence and returns the per-env episode dicts of envs that finished.
+    ``style``: 'logging' writes utils_logging.Monitor's rows (r, l, t,
+    current_reward, episode + info_keywords; utils_logging.py:98-116),
+    'sb' the stable-baselines wrappers.monitor.Monitor's (r, l, t +
+    info_keywords, monitor.py:94-123), whose reset refuses envs still in an
+    episode unless ``allow_early_resets`` (monitor.py:69-75).
     """
 
     def __init__(self, num_envs, file_paths=None, info_keywords=(), chunk_size=1,
-                 callbacks=None):
+                 callbacks=None, style='logging', allow_early_resets=True):
+        if style not in ('logging', 'sb'):
+            raise ValueError('style must be logging or sb')
+        self.style = style
+        self.allow_early_resets = bool(allow_early_resets)
+        self.needs_reset = np.ones(num_envs, bool)
         self.num_envs = num_envs
         if file_paths is None or isinstance(file_paths, (str, Path)):
             file_paths = [file_paths] * num_envs if file_paths is None else [
@@ -138,6 +148,11 @@ class VecMonitor:
 
     def reset(self, indices=None):
         idx = slice(None) if indices is None else indices
+        if self.style == 'sb' and not self.allow_early_resets and not self.needs_reset[idx].all():
+            raise RuntimeError('Tried to reset an environment before done. If you want to '
+                               'allow early resets, wrap your env with Monitor(env, path, '
+                               'allow_early_resets=True)')
+        self.needs_reset[idx] = False
         self.ep_reward[idx] = 0.0
         self.ep_len[idx] = 0
         self.current_episode[idx] += 1
@@ -159,9 +174,12 @@ class VecMonitor:
         now = time.time() - self.t_start
         for i in np.flatnonzero(dones):
             info = infos[i]
+            self.needs_reset[i] = True
             ep_info = {'r': round(float(self.ep_reward[i]), 6), 'l': int(self.ep_len[i]),
-                       't': round(now, 6), 'current_reward': float(rewards[i]),
-                       'episode': int(self.current_episode[i])}
+                       't': round(now, 6)}
+            if self.style == 'logging':
+                ep_info['current_reward'] = float(rewards[i])
+                ep_info['episode'] = int(self.current_episode[i])
             for key in self.info_keywords:
                 ep_info[key] = info[key]
             self.data[i].append(ep_info)

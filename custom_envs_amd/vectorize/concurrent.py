@@ -37,17 +37,31 @@ def spec_key(kwargs):
 
 def monitor_parts(fn):
     """``partial(Monitor, target, path, **kw)`` -> (target, (path, kw)); any
-    other factory -> (fn, None).  The scripts' utils_logging.Monitor
-    (run_multiagent_exp_single.py:78-86, search_optimize_hyperparam.py:
-    99-112); its ``.mon.csv`` rows are what ``VecMonitor`` writes."""
+    other factory -> (fn, None).  Two Monitors are recognised:
+      - the scripts' utils_logging.Monitor (run_multiagent_exp_single.py:
+        78-86, search_optimize_hyperparam.py:99-112): rows r, l, t,
+        current_reward, episode + info_keywords;
+      - the stable-baselines style custom_envs.wrappers.Monitor
+        (wrappers/monitor.py:11-163): rows r, l, t + info_keywords, the
+        reset-before-done check (``allow_early_resets``).  Its
+        ``reset_keywords`` need kwargs a VecEnv reset never passes, so a
+        factory that sets them is not batched (target None).
+    ``VecMonitor`` writes the same ``.mon.csv`` rows in either style."""
     from custom_envs_amd.utils.utils_logging import Monitor
-    if not (isinstance(fn, functools.partial) and fn.func is Monitor):
+    from custom_envs_amd.wrappers.monitor import Monitor as SBMonitor
+    if not (isinstance(fn, functools.partial) and fn.func in (Monitor, SBMonitor)):
         return fn, None
     if not fn.args:
         return None, None
     kw = dict(fn.keywords)
     path = fn.args[1] if len(fn.args) > 1 else kw.pop('file_path', None)
-    kw.pop('allow_early_resets', None)      # run_multiagent_exp_single.py:80
+    if fn.func is SBMonitor:
+        if tuple(kw.pop('reset_keywords', ()) or ()):
+            return None, None
+        kw['style'] = 'sb'
+        kw['allow_early_resets'] = bool(kw.get('allow_early_resets', False))
+    else:
+        kw.pop('allow_early_resets', None)      # run_multiagent_exp_single.py:80
     return fn.args[0], (path, kw)
 
 
@@ -164,9 +178,17 @@ class ConcurrentVecEnv:
         if request is not None:
             from custom_envs_amd.vectorize.gpuvecenv import GPUVecEnv
             kwargs, mon, built = request
-            for env in built:      # single-env engines the caller built eagerly
+            # instances the caller built eagerly (partial(Monitor, make(...)))
+            # are replaced by the batched engine and closed; their seeds carry
+            # over when every factory is such an instance with a seed set
+            seeds = None
+            if built and len(built) == len(env_fns):
+                seeds = [env.engine.seeds[0] for env in built]
+                if any(s is None for s in seeds):
+                    seeds = None
+            for env in built:
                 env.close()
-            self._gpu = GPUVecEnv(len(env_fns), monitor=mon, **kwargs)
+            self._gpu = GPUVecEnv(len(env_fns), monitor=mon, seed=seeds, **kwargs)
             self.num_envs = self._gpu.num_envs
             self.observation_space = self._gpu.observation_space
             self.action_space = self._gpu.action_space

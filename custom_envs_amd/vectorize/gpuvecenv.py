@@ -78,7 +78,9 @@ class GPUVecEnv:
             self.monitor = VecMonitor(self.num_envs, paths,
                                       info_keywords=mkw.get('info_keywords', ()),
                                       chunk_size=mkw.get('chunk_size', 1),
-                                      callbacks=mkw.get('callbacks'))
+                                      callbacks=mkw.get('callbacks'),
+                                      style=mkw.get('style', 'logging'),
+                                      allow_early_resets=mkw.get('allow_early_resets', True))
         self.current_step = np.zeros(self.num_envs, np.int64)
         self.waiting = False
         self.closed = False

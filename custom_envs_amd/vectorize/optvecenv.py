@@ -163,7 +163,9 @@ class OptVecEnv:
                 paths, mkw = mon
                 self.monitor = VecMonitor(E, paths, info_keywords=mkw.get('info_keywords', ()),
                                           chunk_size=mkw.get('chunk_size', 1),
-                                          callbacks=mkw.get('callbacks'))
+                                          callbacks=mkw.get('callbacks'),
+                                          style=mkw.get('style', 'logging'),
+                                          allow_early_resets=mkw.get('allow_early_resets', True))
         else:
             runners = [functools.partial(OptEnvRunner, fn) for fn in environment_fns]
             self._host = ThreadVecEnv(runners)
@@ -258,7 +260,9 @@ class OptVecEnv:
             # 'nn' problem draws its weights and shuffles from these seeds
             from custom_envs_amd.engine import normalize_seed
             seed = method_args[0] if method_args else method_kwargs.get('seed')
-            seeds = list(getattr(self, '_seeds', range(E)))
+            # env i's seed changes only for i in indices: the others keep the
+            # engine's current seeds, however they were set
+            seeds = list(getattr(self._engine, 'seeds', None) or getattr(self, '_seeds', range(E)))
             for i in idx:
                 seeds[i] = normalize_seed(seed)
             self._engine.seed(seeds)

@@ -79,7 +79,7 @@
 extern "C" {
 #endif
 
-#define CE_ABI_VERSION 2
+#define CE_ABI_VERSION 3
 
 typedef struct ce_engine ce_engine;
 
@@ -95,9 +95,13 @@ typedef enum ce_status {
 typedef enum ce_problem {
     /* softmax classifier without bias (the missing ModelNumpy) */
     CE_PROBLEM_SOFTMAX = 0,
-    /* F -> n_hidden (relu) -> K softmax MLP, float32 (OptimizeNN network,
-       custom_envs/problems/optimize_nn.py:35-52);
-       flat parameters [W1 (F,H) | b1 | W2 (H,K) | b2]; CE_F32 only */
+    /* F -> hidden... (relu) -> K softmax network, float32 (OptimizeNN,
+       custom_envs/problems/optimize_nn.py:22-64, create_neural_net
+       utils_tf.py:74-86); flat parameters
+       [W1 | b1 | W2 | b2 | ...] in trainable_variables order; CE_F32 only.
+       One hidden layer of 64 with B = 32 runs the fused config-3 kernel;
+       every other network (1-4 hidden layers, any widths, any B in 1..N,
+       K <= 32) the layered path (net_engine.hip) */
     CE_PROBLEM_MLP = 1
 } ce_problem;
 
@@ -123,8 +127,12 @@ typedef struct ce_config {
     int32_t max_steps;   /* episode length, optimize.py:102-103 (40)        */
     int32_t auto_reset;  /* 1: VecEnv auto-reset on done (utils_venv.py:31);
                             0: single gym.Env (baseenvironment.py:30-41)   */
-    int32_t n_hidden;    /* CE_PROBLEM_MLP hidden units (create_neural_net
-                            layers, utils_tf.py:74-86); ignored otherwise  */
+    int32_t n_hidden;    /* CE_PROBLEM_MLP hidden units of a one-layer
+                            network (create_neural_net layers,
+                            utils_tf.py:74-86); ignored otherwise          */
+    int32_t n_layers;    /* CE_PROBLEM_MLP: 0 = one layer of n_hidden;
+                            1..4 = that many hidden layers, widths below   */
+    int32_t hidden[4];   /* the hidden widths when n_layers > 0            */
 } ce_config;
 
 /* Per-step outputs, one row per env.  obs is [E][2P+1] with P the problem's

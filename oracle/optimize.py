@@ -138,21 +138,29 @@ class ModelNumpy:
 
 
 class ModelMLP:
-    """A12: float32 F -> hidden (relu) -> K (softmax) classifier, flat params."""
+    """A12: float32 F -> hidden... (relu) -> K (softmax) classifier, flat
+    params [W1 | b1 | W2 | b2 | ...] in trainable_variables order
+    (optimize_nn.py:22-64, create_neural_net utils_tf.py:74-86).  ``hidden``:
+    one width (config 3: 64) or a tuple of widths (the reference default
+    (256, 256))."""
 
     def __init__(self, feature_size, num_of_labels, hidden=64):
-        F, H, K = feature_size, hidden, num_of_labels
-        self.dims = (F, H, K)
-        self.shapes = ((F, H), (H,), (H, K), (K,))
-        self.size = F * H + H + H * K + K
+        hidden = (int(hidden),) if np.isscalar(hidden) else tuple(int(h) for h in hidden)
+        self.dims = (feature_size,) + hidden + (num_of_labels,)
+        shapes = []
+        for fan_in, fan_out in zip(self.dims[:-1], self.dims[1:]):
+            shapes += [(fan_in, fan_out), (fan_out,)]
+        self.shapes = tuple(shapes)
+        self.size = int(sum(np.prod(s) for s in self.shapes))
         self.weights = np.zeros(self.size, np.float32)
 
     def reset(self):
-        F, H, K = self.dims
-        w1 = npr.uniform(-np.sqrt(6.0 / (F + H)), np.sqrt(6.0 / (F + H)), (F, H))
-        w2 = npr.uniform(-np.sqrt(6.0 / (H + K)), np.sqrt(6.0 / (H + K)), (H, K))
-        self.weights = np.concatenate([w1.ravel(), np.zeros(H), w2.ravel(),
-                                       np.zeros(K)]).astype(np.float32)
+        """glorot-uniform kernels layer by layer from the global npr, zero biases."""
+        parts = []
+        for fan_in, fan_out in zip(self.dims[:-1], self.dims[1:]):
+            lim = np.sqrt(6.0 / (fan_in + fan_out))
+            parts += [npr.uniform(-lim, lim, (fan_in, fan_out)).ravel(), np.zeros(fan_out)]
+        self.weights = np.concatenate(parts).astype(np.float32)
 
     def set_weights(self, weights):
         self.weights = np.asarray(weights, np.float32).reshape(-1)
@@ -166,17 +174,23 @@ class ModelMLP:
         return out
 
     def compute_backprop(self, features, labels):
-        w1, b1, w2, b2 = self.unflatten()
-        z1 = features @ w1 + b1
-        hid = np.maximum(z1, np.float32(0))
-        prob = softmax(hid @ w2 + b2)
+        params = self.unflatten()
+        kernels, biases = params[0::2], params[1::2]
+        acts, pre = [features], []
+        for w, b in zip(kernels[:-1], biases[:-1]):
+            z = acts[-1] @ w + b
+            pre.append(z)
+            acts.append(np.maximum(z, np.float32(0)))
+        prob = softmax(acts[-1] @ kernels[-1] + biases[-1])
         loss = cross_entropy(prob, labels)
-        dz2 = prob - labels
-        dz1 = (dz2 @ w2.T) * (z1 > 0)
-        grad = np.concatenate([(features.T @ dz1).ravel(), dz1.sum(axis=0),
-                               (hid.T @ dz2).ravel(), dz2.sum(axis=0)])
+        dz = prob - labels
+        grads = []
+        for layer in range(len(kernels) - 1, -1, -1):
+            grads = [(acts[layer].T @ dz).ravel(), dz.sum(axis=0)] + grads
+            if layer > 0:
+                dz = (dz @ kernels[layer].T) * (pre[layer - 1] > 0)
         accuracy = np.mean(np.argmax(prob, axis=1) == np.argmax(labels, axis=1))
-        return loss, grad, accuracy
+        return loss, np.concatenate(grads), accuracy
 
 
 class Optimize:
@@ -269,16 +283,19 @@ class Optimize:
 
 
 def initial_draws_mlp(seed, n_features, hidden, n_classes, n_rows):
-    """(W0 flat float32, perm) of the A12 MLP: uniform W1, uniform W2, then
-    shuffle(arange(N)), all from the env's (never advanced) RandomState."""
+    """(W0 flat float32, perm) of the A12 MLP: glorot-uniform kernels layer by
+    layer, zero biases, then shuffle(arange(N)), all from the env's (never
+    advanced) RandomState.  ``hidden``: a width or a tuple of widths."""
     rng, _ = np_random(seed)
-    F, H, K = n_features, hidden, n_classes
-    w1 = rng.uniform(-np.sqrt(6.0 / (F + H)), np.sqrt(6.0 / (F + H)), (F, H))
-    w2 = rng.uniform(-np.sqrt(6.0 / (H + K)), np.sqrt(6.0 / (H + K)), (H, K))
-    weights = np.concatenate([w1.ravel(), np.zeros(H), w2.ravel(), np.zeros(K)])
+    hidden = (int(hidden),) if np.isscalar(hidden) else tuple(int(h) for h in hidden)
+    dims = (n_features,) + hidden + (n_classes,)
+    parts = []
+    for fan_in, fan_out in zip(dims[:-1], dims[1:]):
+        lim = np.sqrt(6.0 / (fan_in + fan_out))
+        parts += [rng.uniform(-lim, lim, (fan_in, fan_out)).ravel(), np.zeros(fan_out)]
     perm = np.arange(n_rows)
     rng.shuffle(perm)
-    return weights.astype(np.float32), perm
+    return np.concatenate(parts).astype(np.float32), perm
 
 
 def initial_draws(seed, n_features, n_classes, n_rows):

@@ -3,7 +3,7 @@
 # interleaved runs to expose run-to-run noise.
 set -u
 cd "$(dirname "$0")/.."
-OUT=gpurun_out
+OUT=${OUT:-gpurun_out}
 mkdir -p $OUT
 fatal() { case $1 in 0) ;; *) echo "GPU step failed (rc=$1), stopping"; exit $1;; esac; }
 for rep in 1 2; do

@@ -23,7 +23,7 @@ __device__ __forceinline__ void valu_step(double (&v)[16], double b, double cc) 
 }
 
 template <int KIND>
-__global__ __launch_bounds__(512) void k(double *out, double seed) {
+__global__ __launch_bounds__(1024) void k(double *out, double seed) {
     d4 acc[4];
     for (int c = 0; c < 4; ++c) acc[c] = d4{seed, seed, seed, seed};
     double v[16];
@@ -40,7 +40,8 @@ __global__ __launch_bounds__(512) void k(double *out, double seed) {
         if (KIND == 0) mfma_step(acc, a, b);
         if (KIND == 1) valu_step(v, b, cc);
         if (KIND == 2) { mfma_step(acc, a, b); valu_step(v, b, cc); }
-        if (KIND == 3) { if (wave & 1) valu_step(v, b, cc); else mfma_step(acc, a, b); }
+        // waves w and w + 4 share SIMD w % 4 (round-robin placement): one of each kind per SIMD
+        if (KIND == 3) { if ((wave >> 2) & 1) valu_step(v, b, cc); else mfma_step(acc, a, b); }
         if (KIND == 4) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) s4[c] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, s4[c], 0, 0, 0);
@@ -61,15 +62,16 @@ __global__ __launch_bounds__(512) void k(double *out, double seed) {
 
 int main() {
     double *out;
-    hipMalloc(&out, sizeof(double) * 512 * 1024);
+    hipMalloc(&out, sizeof(double) * 1024 * 1024);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     const char *names[] = {"mfma16x16x4", "valu_fma16", "mixed_same_wave", "split_waves", "mfma4x4x4", "lds_table"};
     void (*fns[])(double *, double) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>};
-    for (int wps = 1; wps <= 2; ++wps) {
+    for (int wps = 1; wps <= 4; ++wps) {
         for (int kind = 0; kind < 6; ++kind) {
-            if (kind == 3 && wps == 1) continue;
+            if (kind == 3 && wps != 2) continue;
+            if ((kind == 0 || kind == 2) && wps > 2) continue;
             const int threads = 256 * wps;   // 4 or 8 waves per block, one block per CU
             auto launch = [&] { hipLaunchKernelGGL(fns[kind], dim3(256), dim3(threads), 0, 0, out, 1.0); };
             launch();

@@ -113,3 +113,63 @@ def test_vector_env_surface(lr_dataset):
     obs, rews, dones, infos = venv.step(acts)
     assert obs.shape == (E, 41) and rews.shape == (E,) and len(infos) == E
     venv.close()
+
+
+def test_sb_monitor_factories_batch_into_one_engine(tmp_path, lr_dataset):
+    """The stable-baselines style custom_envs.wrappers.Monitor
+    (wrappers/monitor.py:11-163) around Optimize-v0 factories batches into one
+    engine with a VecMonitor, and writes the same .mon.csv rows (r, l +
+    info_keywords; t is wall time) as per-env wrappers run on host workers."""
+    import pandas as pd
+    import custom_envs
+    from custom_envs.vectorize import ThreadVecEnv
+    from custom_envs.wrappers import Monitor
+    E, T = 4, 83
+    acts = np.random.RandomState(6).normal(0, 0.01, (T, E, 20)).astype(np.float32)
+    outs = {}
+    for kind in ('batched', 'per_env'):
+        paths = [str(tmp_path / ('%s_%d' % (kind, i))) for i in range(E)]
+        if kind == 'batched':
+            fns = [functools.partial(Monitor, custom_envs.make('Optimize-v0', data_set=lr_dataset),
+                                     paths[i], info_keywords=('objective', 'accuracy'))
+                   for i in range(E)]
+        else:                      # a lambda is not a recognised spec: one host worker per env
+            fns = [(lambda p=p: Monitor(custom_envs.make('Optimize-v0', data_set=lr_dataset), p,
+                                        info_keywords=('objective', 'accuracy'))) for p in paths]
+        venv = ThreadVecEnv(fns)
+        assert venv.engine_backed == (kind == 'batched')
+        venv.env_method('seed', 7)
+        venv.reset()
+        infos_done = []
+        for t in range(T):
+            _, rews, dones, infos = venv.step(acts[t])
+            for i in np.flatnonzero(dones):
+                infos_done.append((t, int(i), infos[i]['episode']['l'],
+                                   round(float(infos[i]['episode']['r']), 4)))
+        assert venv.env_method('get_episode_lengths') == [[40, 40]] * E
+        outs[kind] = ([pd.read_csv(p + '.mon.csv') for p in paths], infos_done)
+        venv.close()
+    for a, b in zip(outs['batched'][0], outs['per_env'][0]):
+        assert sorted(a.columns) == sorted(b.columns) == ['accuracy', 'l', 'objective', 'r', 't']
+        assert list(a['l']) == list(b['l']) == [40, 40]
+        np.testing.assert_allclose(a['r'], b['r'], rtol=1e-6)
+        np.testing.assert_allclose(a['objective'], b['objective'], rtol=1e-6)
+        np.testing.assert_array_equal(a['accuracy'], b['accuracy'])
+    assert outs['batched'][1] == outs['per_env'][1]
+
+
+def test_sb_monitor_refuses_early_reset(lr_dataset):
+    """allow_early_resets=False (the SB default): a VecEnv reset in the middle
+    of an episode raises, as the per-env wrapper does (monitor.py:69-75)."""
+    import custom_envs
+    from custom_envs.vectorize import ThreadVecEnv
+    from custom_envs.wrappers import Monitor
+    fns = [functools.partial(Monitor, custom_envs.make('Optimize-v0', data_set=lr_dataset), None)
+           for _ in range(3)]
+    venv = ThreadVecEnv(fns)
+    assert venv.engine_backed
+    venv.reset()
+    venv.step(np.zeros((3, 20), np.float32))
+    with pytest.raises(RuntimeError, match='allow early resets'):
+        venv.reset()
+    venv.close()

@@ -284,3 +284,41 @@ def test_image_shape_full_size():
     assert eng.step_kernel == 'optimize_mfma_kernel<13>'
     _check(ds, None, eng, [0, 7, 8], 42, scale=0.01)
     eng.close()
+
+
+@pytest.mark.parametrize('lr_waves', [4, 8])
+def test_lr_mfma_extreme_logits(lr_waves):
+    """Envs whose weights reach |u| far past the exp's range (actions of scale
+    40 on some envs) next to ordinary ones: workgroups whose |u| bound stays
+    below 650 run the row loop without the argument clamp, the others with it
+    (CE_LR_NOCLAMP); p_y + 1e-16 and q must match the oracle's max-subtracted
+    softmax either way, including p_y underflowing to 0."""
+    ds = _two_class(256, 10, 21)
+    E, T = 40, 42
+    eng = _engine(ds, E, None, lr=True, lr_waves=lr_waves)
+    P = eng.act_dim
+    scale = np.where(np.arange(E) >= 32, 40.0, 0.01)          # the last group: huge weights
+    scale[5] = 40.0                                            # and one env in the first group
+    acts = (np.random.RandomState(4).normal(0, 1, (T, E, P)) * scale[None, :, None]).astype(np.float32)
+    seeds = [300 + i for i in range(E)]
+    eng.seed(seeds)
+    eng.reset()
+    check = [0, 5, 16, 31, 32, 39]
+    refs = {}
+    for i in check:
+        env = OracleEnv(*ds)
+        env.seed(seeds[i])
+        env.reset()
+        refs[i] = env
+    for t in range(T):
+        out = eng.step(acts[t])
+        for i, env in refs.items():
+            obs, rew, done, info = env.step(acts[t, i])
+            if done:
+                obs = env.reset()
+            assert bool(out['done'][i]) == done
+            np.testing.assert_allclose(out['obs'][i], obs, rtol=1e-6, atol=1e-9,
+                                       err_msg='env %d step %d' % (i, t))
+            assert out['reward'][i] == pytest.approx(rew, rel=1e-6)
+            assert out['accuracy'][i] == np.float32(info['accuracy'])
+    eng.close()

@@ -260,3 +260,102 @@ def test_fused_step_matches_split_kernels(monkeypatch):
     finally:
         fused.close()
         split.close()
+
+
+# ---------------------------------------------------------------------------
+# The layered network path (net_engine.hip): Optimize-v0 over any OptimizeNN
+# network (create_neural_net's default (256, 256), optimize_nn.py:22-64,
+# utils_tf.py:74-86) and any batch size.  Same tolerances as above; accuracy
+# may differ by one row where two float32 probabilities tie to rounding.
+
+def _net_engine(features, targets, num_envs, hidden, batch_size, monkeypatch=None, force=False):
+    from custom_envs_amd.engine import OptimizeEngine
+    if force:
+        monkeypatch.setenv('CE_MLP_NET', '1')
+    eng = OptimizeEngine(features, targets, num_envs=num_envs, batch_size=batch_size, model='mlp',
+                         hidden=hidden)
+    if force:
+        monkeypatch.delenv('CE_MLP_NET')
+    return eng
+
+
+def _net_check(features, targets, eng, hidden, batch_size, seeds, steps, scale=1e-3):
+    refs = []
+    for s in seeds:
+        env = OracleEnv(features, targets, batch_size=batch_size, model='mlp', hidden=hidden)
+        env.seed(s)
+        env.reset()
+        refs.append(env)
+    eng.seed(seeds)
+    assert np.all(eng.reset() == 0)
+    P = eng.act_dim
+    assert P == refs[0].model.size
+    n_rows = len(features)
+    rs = np.random.RandomState(len(seeds) + P)
+    for t in range(steps):
+        acts = rs.normal(0, scale, (len(seeds), P)).astype(np.float32)
+        out = eng.step(acts)
+        weights = eng.get_state()['weights'].astype(np.float32)
+        for i, env in enumerate(refs):
+            obs, reward, done, info = env.step(acts[i])
+            if not done:     # W <- W - a is one float32 subtraction on both sides
+                assert np.array_equal(weights[i], env.model.weights), (i, t)
+            if done:
+                obs = env.reset()
+            assert bool(out['done'][i]) == done, (i, t)
+            assert int(out['episode_len'][i]) == info['episode']['l']
+            assert not out['obs'][i][:P].any()
+            _row_close(out['obs'][i], obs)
+            assert _rel(out['reward'][i], reward) <= RTOL, (i, t)
+            assert _rel(out['objective'][i], info['objective']) <= RTOL, (i, t)
+            assert abs(float(out['accuracy'][i]) - info['accuracy']) <= 1.5 / n_rows, (i, t)
+
+
+@pytest.mark.parametrize('batch_size', [16, 32, 100])
+def test_default_network_256x256(batch_size):
+    """create_neural_net's default layers (256, 256) over the MNIST-sized set
+    (1024 x 784, 10 classes): P = 269,322; 3 envs across an auto-reset; B of
+    16, 32 and 100 (a batch that is not a multiple of anything)."""
+    from custom_envs_amd.data import load_data
+    seq = load_data('mnist_synthetic', batch_size=batch_size)
+    eng = _net_engine(seq.features, seq.targets, 3, (256, 256), batch_size)
+    try:
+        assert eng.step_kernel == 'net<784,256,256,10>'
+        _net_check(seq.features, seq.targets, eng, (256, 256), batch_size, [3, 4, 5], 42)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize('hidden,batch_size', [((96, 32, 48), 20), ((40,), None), ((64,), 32)])
+def test_network_shapes(hidden, batch_size, monkeypatch):
+    """Three hidden layers, one layer with the full batch (B = N: the info pass
+    reuses the minibatch numbers), and config 3's shape forced onto the
+    layered path (CE_MLP_NET=1) -- 5 envs, one mid-episode reset crossed."""
+    from oracle.gen_golden import mlp_dataset
+    features, targets = mlp_dataset()
+    force = hidden == (64,)
+    eng = _net_engine(features, targets, 5, hidden, batch_size, monkeypatch, force=force)
+    try:
+        assert eng.step_kernel.startswith('net<')
+        _net_check(features, targets, eng, hidden, batch_size, [7, 8, 9, 10, 11], 43, scale=3e-3)
+    finally:
+        eng.close()
+
+
+def test_network_seed_draws_match_numpy():
+    """W0 of a two-layer network: glorot-uniform per layer then the reset
+    shuffle on the same stream (oracle.initial_draws_mlp)."""
+    from custom_envs_amd.data import load_data
+    from oracle.optimize import initial_draws_mlp
+    seq = load_data('mnist_synthetic', batch_size=32)
+    eng = _net_engine(seq.features, seq.targets, 2, (256, 256), 32)
+    try:
+        eng.seed([11, 12])
+        eng.reset()
+        st = eng.get_state()
+        for i, s in enumerate((11, 12)):
+            w0, perm = initial_draws_mlp(s, 784, (256, 256), 10, 1024)
+            assert np.array_equal(st['init_weights'][i].astype(np.float32), w0)
+            assert np.array_equal(st['order'][i], perm)
+    finally:
+        eng.close()

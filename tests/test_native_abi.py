@@ -35,8 +35,9 @@ def test_every_declared_symbol_is_exported():
 def test_config_struct_matches_header():
     text = open(os.path.join(ROOT, 'include', 'custom_envs_amd.h')).read()
     body = text[text.index('typedef struct ce_config'):text.index('} ce_config;')]
-    fields = re.findall(r'int32_t\s+(\w+);', body)
+    fields = re.findall(r'int32_t\s+(\w+)(?:\[\d+\])?;', body)
     assert fields == [f[0] for f in _native.CeConfig._fields_]
+    assert ctypes.sizeof(_native.CeConfig) == 4 * (len(fields) - 1) + 4 * 4   # hidden[4]
 
 
 def test_native_seeding_matches_numpy_and_hashlib():
@@ -116,10 +117,13 @@ def test_native_mlp_seeding_against_live_numpy(seed):
     assert np.array_equal(w0, w_ref) and np.array_equal(perm, p_ref)
 
 
-@pytest.mark.parametrize('change', [dict(n_hidden=32), dict(batch_size=16),
-                                    dict(n_features=20), dict(n_classes=17),
+@pytest.mark.parametrize('change', [dict(n_classes=33), dict(n_layers=5),
                                     dict(precision=_native.CE_F64)])
 def test_unsupported_mlp_shape_is_loud(change):
+    """Networks the engine does not run (more than 32 classes, more than 4
+    hidden layers, float64) fail at ce_create before any HIP call; every
+    other width / depth / batch size runs (the fused config-3 kernel or the
+    layered path)."""
     lib = _native.load()
     base = dict(abi_version=_native.ABI_VERSION, problem=_native.CE_PROBLEM_MLP,
                 precision=_native.CE_F32, num_envs=1, n_rows=128, n_features=16,
