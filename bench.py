@@ -128,6 +128,9 @@ def parse(argv=None):
     p.add_argument('--workload', default='optimize',
                    choices=['optimize', 'multi', 'mlp', 'nn', 'mnist'])
     p.add_argument('--precision', default='f64', choices=['f64', 'f32'])
+    p.add_argument('--hidden', default='64',
+                   help='mlp workload: hidden widths, e.g. 256,256 (create_neural_net default)')
+    p.add_argument('--batch-size', type=int, default=32, help='mlp workload: minibatch rows')
     p.add_argument('--graph-steps', type=int, default=250, help='steps per hipGraph replay')
     p.add_argument('--no-gather', action='store_true',
                    help='N > 1: no per-step all-gather in the headline value')
@@ -143,6 +146,7 @@ def parse(argv=None):
     p.add_argument('--profile-only', action='store_true',
                    help='run the timed steps only (for rocprofv3)')
     args = p.parse_args(argv)
+    args.hidden = tuple(int(h) for h in str(args.hidden).split(',') if h)
     if args.workload == 'mnist' and '--steps' not in (argv or sys.argv):
         args.steps, args.warmup = 30, 3      # ~13 ms per step at 4096 envs
     if args.envs is None:
@@ -357,8 +361,8 @@ def build_mlp(args, torch, device, rank, world, phases=None):
     if phases:
         os.environ['CE_MLP_PHASES'] = phases
     try:
-        eng = OptimizeEngine(features, targets, num_envs=E, batch_size=32, model='mlp',
-                             device=device)
+        eng = OptimizeEngine(features, targets, num_envs=E, batch_size=args.batch_size,
+                             model='mlp', hidden=args.hidden, device=device)
     finally:
         os.environ.pop('CE_MLP_PHASES', None)
     eng.seed([rank * E + i for i in range(E)])
@@ -368,7 +372,7 @@ def build_mlp(args, torch, device, rank, world, phases=None):
     return eng, actions, S
 
 
-def cpu_baseline_mlp(envs, budget_s):
+def cpu_baseline_mlp(envs, budget_s, hidden=(64,), batch_size=32):
     """Oracle float32 MLP Optimize envs under the restated ThreadVecEnv."""
     from oracle.optimize import Optimize as OracleEnv
     from oracle.vectorize import ThreadVecEnv
@@ -377,21 +381,24 @@ def cpu_baseline_mlp(envs, budget_s):
 
     def factory(seed):
         def make():
-            env = OracleEnv(features, targets, batch_size=32, model='mlp')
+            env = OracleEnv(features, targets, batch_size=batch_size, model='mlp', hidden=hidden)
             env.seed(seed)
             return env
         return make
 
     venv = ThreadVecEnv([factory(i) for i in range(n)])
     venv.reset()
-    acts = np.random.RandomState(0).normal(0, 1e-3, (n, 50890)).astype(np.float32)
+    n_params = venv.get_attr('obs_size')[0] // 2
+    acts = np.random.RandomState(0).normal(0, 1e-3, (n, n_params)).astype(np.float32)
     steps, wall, cpu = _time_cpu(venv, acts, budget_s)
     venv.close()
+    dims = '-'.join(map(str, (784,) + tuple(hidden) + (10,)))
     return {'value': n * steps / wall, 'unit': 'env-steps/s',
             'cores': max(1, int(round(cpu / wall))), 'kind': 'port',
             'sample': '%d envs x %d steps of ThreadVecEnv over the numpy oracle Optimize env '
-                      'with the float32 784-64-10 MLP (BLAS sgemm); %.1f s wall, %.1f s CPU; '
-                      'os.cpu_count()=%d' % (n, steps, wall, cpu, os.cpu_count())}
+                      'with the float32 %s network, B=%d (BLAS sgemm); %.1f s wall, %.1f s CPU; '
+                      'os.cpu_count()=%d' % (n, steps, dims, batch_size, wall, cpu,
+                                              os.cpu_count())}
 
 
 def build_multi(args, torch, device, rank, world):
@@ -448,7 +455,8 @@ def run_cpu_baseline_child(args):
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), '--cpu-baseline-only',
            '--workload', args.workload, '--envs', str(args.envs),
-           '--cpu-seconds', str(args.cpu_seconds)]
+           '--cpu-seconds', str(args.cpu_seconds),
+           '--hidden', ','.join(map(str, args.hidden)), '--batch-size', str(args.batch_size)]
     res = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     for line in reversed(res.stdout.splitlines()):
         if line.startswith('{'):
@@ -465,7 +473,7 @@ def cpu_baseline_only(args):
     elif args.workload == 'multi':
         cpu = cpu_baseline_multi(args.envs, args.cpu_seconds)
     elif args.workload == 'mlp':
-        cpu = cpu_baseline_mlp(args.envs, args.cpu_seconds)
+        cpu = cpu_baseline_mlp(args.envs, args.cpu_seconds, args.hidden, args.batch_size)
     else:
         cpu = cpu_baseline(*lr_dataset(), args.envs, args.cpu_seconds)
     cpu.setdefault('host', host_info())
@@ -698,7 +706,7 @@ def main():
     times = [a.elapsed_time(b) / S for a, b in zip(starts, ends)]
     kernel_ms, kernel_ms_mean = float(np.median(times)), float(np.mean(times))
     phase_ms = {}
-    if mlp and rank == 0:
+    if mlp and rank == 0 and not eng.step_kernel.startswith('net<'):
         # each MLP kernel alone (CE_MLP_PHASES engines), same events method
         for phase in ('train', 'info'):
             peng, pact, _ = build_mlp(args, torch, device, rank, world, phases=phase)
@@ -724,7 +732,9 @@ def main():
         host_rate = host_loop_rate(args, device, E)
 
     if rank == 0:
-        if mlp:
+        if mlp and eng.step_kernel.startswith('net<'):
+            line = net_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard)
+        elif mlp:
             line = mlp_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard,
                             phase_ms)
         elif nn:
@@ -937,6 +947,54 @@ def mnist_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean):
                      'kernel_ms_mean': kernel_ms_mean,
                      'note': 'algorithmic GEMM flops; the kernel pads K 10 -> 16 and F 49 -> '
                              '52 (forward) / 64 (gradient) on 16x16x4 MFMA tiles'},
+    })
+    return line
+
+
+def net_flops(dims, B, N):
+    """Algorithmic FLOPs of one Optimize-v0 step over the network dims (F,
+    hidden..., K): minibatch forward 2B sum(d_l d_l+1), backward dW 2B
+    sum(d_l d_l+1) and dH 2B sum_{l>0}(d_l d_l+1); the full-data info forward
+    2N sum(d_l d_l+1) when B < N (B == N reuses the minibatch pass)."""
+    pairs = [a * b for a, b in zip(dims[:-1], dims[1:])]
+    train = 2 * B * (2 * sum(pairs) + sum(pairs[1:]))
+    info = 2 * N * sum(pairs) if B < N else 0
+    return train, info
+
+
+def net_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
+    """The layered network path: every layer's product is a strided-batched
+    rocBLAS sgemm over the envs (MFMA), the rest hand-written kernels; the
+    roofline is the MFMA rate over the step's algorithmic FLOPs."""
+    dims = (784,) + tuple(args.hidden) + (10,)
+    P = eng.act_dim
+    train_f, info_f = net_flops(dims, args.batch_size, 1024)
+    achieved = (train_f + info_f) * E / (kernel_ms * 1e-3) / 1e12
+    line = {'metric': METRIC_MLP.replace('784-64-10 MLP', '-'.join(map(str, dims)) + ' network')}
+    line.update(_common(args, world, E, S, elapsed, shard))
+    line.update({
+        'dtype': 'f32',
+        'data': 'synthetic: RandomState(0).rand(1024, 784), labels argmax(X T), '
+                'T = RandomState(1).normal(784, 10); glorot-uniform init per env seed; '
+                'actions N(0, 1e-3) float32 generated on device',
+        'config': {
+            'workload': 'Optimize-v0 over the %s relu network (P=%d, obs %d), %d envs per GPU, '
+                        'B=%d of N=1024, full-data info pass every step, auto-reset, '
+                        'device-resident actions/outputs' % ('-'.join(map(str, dims)), P,
+                                                             2 * P + 1, E, args.batch_size),
+            'envs_per_gpu': E, 'global_envs': world * E, 'n_rows': 1024, 'n_features': 784,
+            'hidden': list(args.hidden), 'n_classes': 10, 'batch_size': args.batch_size,
+            'parallelism': 'env-sharded x%d (no collective)' % world,
+        },
+        'roofline': {
+            'bound': 'mfma', 'achieved': achieved, 'peak': MFMA_F32_PEAK_TFLOPS,
+            'unit': 'TFLOP/s', 'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': None,
+            'kernel': 'one step = %s: strided-batched rocBLAS sgemm per layer (forward, dW, '
+                      'dH, info forward) + net_update/gather/bias_act/softmax/colsum/relu_back/'
+                      'epilogue/finish kernels' % eng.step_kernel,
+            'flops_per_env_step': train_f + info_f, 'info_flops_per_env_step': info_f,
+            'step_ms_median': kernel_ms, 'step_ms_mean': kernel_ms_mean,
+        },
     })
     return line
 

@@ -37,12 +37,15 @@ def _engine(features, targets, num_envs, auto_reset=True):
                           auto_reset=auto_reset)
 
 
-def _row_close(got, ref, tol=RTOL):
+def _row_close(got, ref, tol=RTOL, what=''):
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
     scale = max(np.abs(ref).max(), 1e-30)
-    err = np.abs(got - ref).max() / scale
-    assert err <= tol, err
+    diff = np.abs(got - ref)
+    err = diff.max() / scale
+    i = int(diff.argmax())
+    assert err <= tol, '%s err %.3g at %d of %d: got %r ref %r (row max %.4g at %d)' % (
+        what, err, i, len(ref), got[i], ref[i], scale, int(np.abs(ref).argmax()))
 
 
 def _rel(got, ref):
@@ -279,7 +282,32 @@ def _net_engine(features, targets, num_envs, hidden, batch_size, monkeypatch=Non
     return eng
 
 
+def _relu_ties(model, weights, X, rel=2e-6):
+    """True when some hidden pre-activation of this minibatch lies within
+    float32 rounding of zero (|z| < rel * sum_k |x_k w_k| + |b|): the two
+    float32 evaluations (BLAS and the engine's GEMMs, summing in different
+    orders) may then take different sides of the relu kink, which moves the
+    gradient of that unit by one sample's term."""
+    h = np.asarray(X, np.float32)
+    start = 0
+    dims = model.dims
+    for din, dout in zip(dims[:-2], dims[1:-1]):
+        w = weights[start:start + din * dout].reshape(din, dout)
+        b = weights[start + din * dout:start + din * dout + dout]
+        start += din * dout + dout
+        z = h @ w + b
+        mag = np.abs(h) @ np.abs(w) + np.abs(b)
+        if np.any(np.abs(z) < rel * mag):
+            return True
+        h = np.maximum(z, 0)
+    return False
+
+
 def _net_check(features, targets, eng, hidden, batch_size, seeds, steps, scale=1e-3):
+    """Tolerances as for config 3.  At a step whose minibatch has a relu tie
+    (_relu_ties) the observation row is checked against the tie-free part:
+    at most 0.1 % of its entries may exceed the tolerance (one unit's
+    column of one layer), and the reward / objective checks stay exact."""
     refs = []
     for s in seeds:
         env = OracleEnv(features, targets, batch_size=batch_size, model='mlp', hidden=hidden)
@@ -292,11 +320,13 @@ def _net_check(features, targets, eng, hidden, batch_size, seeds, steps, scale=1
     assert P == refs[0].model.size
     n_rows = len(features)
     rs = np.random.RandomState(len(seeds) + P)
+    ties = 0
     for t in range(steps):
         acts = rs.normal(0, scale, (len(seeds), P)).astype(np.float32)
         out = eng.step(acts)
         weights = eng.get_state()['weights'].astype(np.float32)
         for i, env in enumerate(refs):
+            tie = _relu_ties(env.model, env.model.weights - acts[i], env.sequence[0][0])
             obs, reward, done, info = env.step(acts[i])
             if not done:     # W <- W - a is one float32 subtraction on both sides
                 assert np.array_equal(weights[i], env.model.weights), (i, t)
@@ -305,10 +335,17 @@ def _net_check(features, targets, eng, hidden, batch_size, seeds, steps, scale=1
             assert bool(out['done'][i]) == done, (i, t)
             assert int(out['episode_len'][i]) == info['episode']['l']
             assert not out['obs'][i][:P].any()
-            _row_close(out['obs'][i], obs)
+            if tie and not done:
+                ties += 1
+                scale_r = max(np.abs(obs).max(), 1e-30)
+                bad = np.abs(out['obs'][i].astype(np.float64) - obs) > RTOL * scale_r
+                assert bad.mean() <= 1e-3, (i, t, int(bad.sum()))
+            else:
+                _row_close(out['obs'][i], obs, what='env %d step %d' % (i, t))
             assert _rel(out['reward'][i], reward) <= RTOL, (i, t)
             assert _rel(out['objective'][i], info['objective']) <= RTOL, (i, t)
             assert abs(float(out['accuracy'][i]) - info['accuracy']) <= 1.5 / n_rows, (i, t)
+    return ties
 
 
 @pytest.mark.parametrize('batch_size', [16, 32, 100])
