@@ -945,8 +945,12 @@ def mnist_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean):
                      'traffic': None, 'kernel': 'ce::' + eng.step_kernel,
                      'flops_per_env_step': flops, 'kernel_ms_median': kernel_ms,
                      'kernel_ms_mean': kernel_ms_mean,
-                     'note': 'algorithmic GEMM flops; the kernel pads K 10 -> 16 and F 49 -> '
-                             '52 (forward) / 64 (gradient) on 16x16x4 MFMA tiles'},
+                     'note': ('algorithmic GEMM flops; the class-concatenated kernel puts the '
+                              '8 envs x 10 classes of a workgroup on 5 MFMA tiles of 16 (no class '
+                              'padding) and the 49th feature on the VALU'
+                              if 'cat' in eng.step_kernel else
+                              'algorithmic GEMM flops; the kernel pads K 10 -> 16 and F 49 -> '
+                              '52 (forward) / 64 (gradient) on 16x16x4 MFMA tiles')},
     })
     return line
 

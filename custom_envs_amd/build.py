@@ -76,6 +76,11 @@ def _compile(out, tmp, defines, verbose):
         obj = os.path.join(tmp, os.path.basename(src) + '.o')
         if src.endswith('.hip'):
             cmd = [hipcc, '--offload-arch=' + ARCH, '-x', 'hip'] + common + ['-c', src, '-o', obj]
+            if os.path.basename(src) == 'optimize_mfma.hip' and 'CE_AGPR_FORM' not in defines:
+                # f64 MFMA results in VGPRs: the two-class kernel's softmax reads
+                # every forward C register, and the AGPR form cost 200
+                # v_accvgpr moves per wave
+                cmd[-4:-4] = ['-mllvm', '-amdgpu-mfma-vgpr-form=1']
         else:
             cmd = [hipcc, '-x', 'c++'] + common + ['-c', src, '-o', obj]
         if verbose:

@@ -130,6 +130,7 @@ struct ce_engine {
     int many_direct = 32;
     int lr_waves = 0;         // CE_LR_WAVES: force the two-class MFMA kernel's wave count
     int gen_tail = 1;         // CE_GEN_TAIL=0: the runtime-shape kernel's last feature on MFMA too
+    int gen_cat = 1;          // CE_GEN_CAT=0: full batch on the one-env-per-wave kernel
     int lr_mode_cap = 3;      // CE_LR_MODE: cap on the two-class MFMA kernel's row-loop mode
     bool compact = false;     // ce_set_compact_outputs: device-pointer calls write the compact form
     unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
@@ -181,6 +182,7 @@ ce::StepArgs<T> make_args(const ce_engine *e, const float *act, const ce_outputs
     a.p_mul = (65536 + P - 1) / P;
     a.lr_waves = e->lr_waves;
     a.gen_tail = e->gen_tail;
+    a.gen_cat = e->gen_cat;
     a.lr_mode_cap = e->lr_mode_cap;
     a.obs_stride = compact ? P + 1 : 2 * P + 1;
     a.obs_lo = compact ? P : 0;
@@ -502,6 +504,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
     if (const char *md = std::getenv("CE_MANY_DIRECT")) e->many_direct = std::atoi(md);
     if (const char *lw = std::getenv("CE_LR_WAVES")) e->lr_waves = std::atoi(lw);
     if (const char *gt = std::getenv("CE_GEN_TAIL")) e->gen_tail = std::atoi(gt);
+    if (const char *gc = std::getenv("CE_GEN_CAT")) e->gen_cat = std::atoi(gc);
     if (const char *lm = std::getenv("CE_LR_MODE")) e->lr_mode_cap = std::atoi(lm);
     // experiment switch: launch one phase only, to time each kernel alone
     if (const char *ph = std::getenv("CE_MLP_PHASES")) {
@@ -643,8 +646,8 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         if (hipMemcpy(e->X, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice) !=
             hipSuccess)
             return bail(fail(CE_EHIP, "ce_create: dataset upload failed"));
-        e->kernel_name =
-            "optimize_mfma_kernel<" + std::to_string((cfg->n_features + 3) / 4) + ">";
+        e->kernel_name = ce::gen_kernel_name(cfg->num_envs, cfg->n_rows, cfg->batch_size,
+                                             cfg->n_features, cfg->n_classes, e->gen_cat);
     } else if (!mlp) {
     // [rows | labels]: row-major rows padded to ce::row_stride elements (zeros
     // in the pad), then the int32 labels, in one buffer staged with one copy.

@@ -94,6 +94,7 @@ struct StepArgs {
     int p_mul;                  // ceil(65536 / P): j = (t p_mul) >> 16 = t / P for t < 2^9
     int lr_waves;               // two-class MFMA kernel: 0 = pick per launch, 4 / 8 = forced
     int gen_tail;               // runtime-shape MFMA kernel: last feature on the VALU when F % 16 == 1
+    int gen_cat;                // full batch: the class-concatenated kernel where it is compiled
     int lr_mode_cap;            // two-class MFMA kernel: cap on the row-loop mode (3 = none)
     int obs_stride;             // floats per obs row: 2P + 1, or P + 1 in the compact form
     int obs_lo;                 // first obs entry stored: 0, or P (compact: the wght_hist

@@ -390,7 +390,12 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
                 const bool valid = !PAD || ys[q] >= 0;
                 qv[q] = valid ? tx[i] * inv : 0.0;
                 prod *= valid ? inv + 1e-16 : 1.0;
-                umin = fmin(umin, valid ? fabs(uq) : 1.0);
+                // min(umin, |u|) as one v_min_f64 with the abs modifier (fmin of
+                // an MFMA result gets a canonicalising v_max_f64 first)
+                {
+                    const double au = valid ? uq : 1.0;
+                    asm("v_min_f64 %0, %1, |%2|" : "=v"(umin) : "v"(umin), "v"(au));
+                }
                 hits += (valid && uq > 0.0) ? 1 : 0;
             }
         }

@@ -20,6 +20,9 @@ int gen_rows_padded_of(int n_rows);
 int gen_set_lds_limits();
 void gen_launch_step(const StepArgs<double> &a, hipStream_t stream);
 void gen_launch_reset(const StepArgs<double> &a, hipStream_t stream);
+// The instance gen_launch_step runs for this shape (as rocprof names it)
+std::string gen_kernel_name(int n_envs, int n_rows, int batch, int n_features, int n_classes,
+                            int gen_cat);
 
 // Two-class, full-batch, F <= 16 (optimize_lr_mfma.h): 16 envs per workgroup
 // on the MFMA N dimension.  The dataset image is fragment-ordered

@@ -3,6 +3,7 @@
 #include "optimize_mfma.h"
 
 #include "common.h"
+#include "optimize_cat_kernel.h"
 #include "optimize_lr_mfma.h"
 #include "optimize_mfma_kernel.h"
 
@@ -17,8 +18,46 @@ namespace {
 
 using GenFn = void (*)(const StepArgs<double> &, hipStream_t);
 
+// The class-concatenated full-batch kernel (optimize_cat_kernel.h), compiled
+// for the shapes listed in kCatShapes; gen_cat = 0 (CE_GEN_CAT=0) keeps the
+// one-env-per-wave kernel.
+template <int NK, bool TAIL, int K>
+void launch_cat(const StepArgs<double> &a, hipStream_t stream) {
+    const int grid = (a.E + kCatEnvs - 1) / kCatEnvs;
+    hipLaunchKernelGGL((optimize_cat_kernel<NK, TAIL, K>), dim3(grid), dim3(kCatBlock),
+                       cat_lds_bytes((NK + 3) / 4, cat_mt(K)), stream, a);
+}
+struct CatShape {
+    int nk, tail, k;
+    GenFn fn;
+    const void *kernel;
+    size_t lds;
+};
+#define CE_CAT(NK, TAIL, K)                                                                   \
+    {NK, TAIL, K, launch_cat<NK, TAIL, K>,                                                   \
+     reinterpret_cast<const void *>(optimize_cat_kernel<NK, TAIL, K>),                       \
+     cat_lds_bytes((NK + 3) / 4, cat_mt(K))}
+// the reference's image sets (49 features, 10 classes) and the smaller
+// shapes that exercise the same paths in tests (no tail, class padding)
+const CatShape kCatShapes[] = {CE_CAT(13, true, 10), CE_CAT(5, true, 10), CE_CAT(4, false, 10),
+                               CE_CAT(3, false, 3), CE_CAT(8, false, 16)};
+#undef CE_CAT
+
+const CatShape *find_cat(const StepArgs<double> &a) {
+    const int nk = (a.F + 3) / 4;
+    const int tail = a.F == 4 * (nk - 1) + 1 && nk % 4 == 1 && nk > 1 ? 1 : 0;
+    for (const auto &c : kCatShapes)
+        if (c.nk == nk && c.tail == tail && c.k == a.K) return &c;
+    return nullptr;
+}
+
 template <int NK>
 void launch_nk(const StepArgs<double> &a, hipStream_t stream) {
+    if (a.B == a.N && a.gen_cat)
+        if (const CatShape *c = find_cat(a)) {
+            c->fn(a, stream);
+            return;
+        }
     const int grid = (a.E + kGenWaves - 1) / kGenWaves;
     // F = 16 (FT - 1) + 1 with the full data set: the last feature on the VALU
     if constexpr (NK % 4 == 1 && NK > 1) {
@@ -151,7 +190,28 @@ std::string lr_kernel_name(int n_envs, int n_rows, int n_features, int lr_waves,
 
 int gen_stride_of(int n_features) { return gen_stride(gen_ft(n_features)); }
 int gen_rows_padded_of(int n_rows) { return gen_rows_padded(n_rows); }
-int gen_set_lds_limits() { return Gen::set_lds_limits(); }
+int gen_set_lds_limits() {
+    for (const auto &c : kCatShapes)
+        CE_HIP(hipFuncSetAttribute(c.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   static_cast<int>(c.lds)));
+    return Gen::set_lds_limits();
+}
+
+std::string gen_kernel_name(int n_envs, int n_rows, int batch, int n_features, int n_classes,
+                            int gen_cat) {
+    (void)n_envs;
+    StepArgs<double> a{};
+    a.N = n_rows;
+    a.B = batch;
+    a.F = n_features;
+    a.K = n_classes;
+    const int nk = (n_features + 3) / 4;
+    if (batch == n_rows && gen_cat)
+        if (const CatShape *c = find_cat(a))
+            return "optimize_cat_kernel<" + std::to_string(nk) + "," + (c->tail ? "true" : "false") +
+                   "," + std::to_string(n_classes) + ">";
+    return "optimize_mfma_kernel<" + std::to_string(nk) + ">";
+}
 
 void gen_launch_step(const StepArgs<double> &a, hipStream_t stream) {
     Gen::steps[(a.F + 3) / 4 - 1](a, stream);

@@ -25,11 +25,13 @@ def _need_gpu():
 
 
 def _engine(dataset, num_envs, batch_size=None, generic=False, lr=False, lr_waves=0, gen_tail=1,
-            lr_mode=3, **kw):
+            lr_mode=3, cat=False, **kw):
+    """cat=False keeps full-batch shapes on the one-env-per-wave kernel
+    (CE_GEN_CAT=0); cat=True lets the class-concatenated kernel take them."""
     from custom_envs_amd.engine import OptimizeEngine
     flags = {'CE_GENERIC': '1' if generic else '0', 'CE_LR_MFMA': '1' if lr else '0',
              'CE_LR_WAVES': str(lr_waves), 'CE_GEN_TAIL': str(gen_tail),
-             'CE_LR_MODE': str(lr_mode)}
+             'CE_LR_MODE': str(lr_mode), 'CE_GEN_CAT': '1' if cat else '0'}
     old = {k: os.environ.get(k) for k in flags}
     os.environ.update(flags)
     try:
@@ -86,7 +88,8 @@ def test_mnist_idx_fixture_through_make():
     from custom_envs_amd.data import load_data
     data_dir = os.path.join(GOLDEN, 'idx')
     env = make('Optimize-v0', data_set='mnist', data_dir=data_dir)
-    assert env.engine.step_kernel == 'optimize_mfma_kernel<13>'   # NK = ceil(49 / 4)
+    # NK = ceil(49 / 4); the full batch of the 8-env class-concatenated kernel
+    assert env.engine.step_kernel == 'optimize_cat_kernel<13,true,10>'
     assert env.observation_space.shape == (2 * 490 + 1,) and env.action_space.shape == (490,)
     seq = load_data('mnist', batch_size=None, data_dir=data_dir)
     ref = OracleEnv(seq.features, seq.targets)
@@ -280,10 +283,50 @@ def test_image_shape_full_size():
     seq = load_data('mnist7x7_synthetic', batch_size=None)
     ds = (seq.features, seq.targets)
     assert ds[0].shape == (60000, 49) and ds[1].shape == (60000, 10)
-    eng = _engine(ds, 9, None)
-    assert eng.step_kernel == 'optimize_mfma_kernel<13>'
-    _check(ds, None, eng, [0, 7, 8], 42, scale=0.01)
+    for cat, kernel in ((True, 'optimize_cat_kernel<13,true,10>'), (False, 'optimize_mfma_kernel<13>')):
+        eng = _engine(ds, 9, None, cat=cat)
+        assert eng.step_kernel == kernel
+        _check(ds, None, eng, [0, 7, 8], 42, scale=0.01)
+        eng.close()
+
+
+@pytest.mark.parametrize('shape', [(49, 10, 1000), (17, 10, 300), (16, 10, 203), (12, 3, 300),
+                                   (32, 16, 130)])
+def test_class_concatenated_kernel(shape):
+    """The full-batch class-concatenated kernel (optimize_cat_kernel.h) at
+    every compiled shape: the image sets' 49 x 10 with a ragged last row
+    block (N = 1000), the VALU tail at F = 17, no tail (F = 16), class
+    padding in the last tile (K = 3: 24 class-pairs in 2 tiles of 16) and
+    K = 16; 13 envs (a full 8-env workgroup and a partial one), across an
+    auto-reset."""
+    F, K, N = shape
+    ds = _classes(N, F, K, F + K + N)
+    eng = _engine(ds, 13, None, cat=True)
+    nk = (F + 3) // 4
+    tail = 'true' if F == 4 * (nk - 1) + 1 and nk % 4 == 1 and nk > 1 else 'false'
+    assert eng.step_kernel == 'optimize_cat_kernel<%d,%s,%d>' % (nk, tail, K)
+    _check(ds, None, eng, [0, 7, 8, 12], 43)
     eng.close()
+
+
+def test_class_concatenated_agrees_with_per_env_kernel():
+    """The same 12 envs through both full-batch kernels: float64 results
+    agree to float32 rounding, done / episode length / accuracy exactly."""
+    ds = _classes(640, 49, 10, 3)
+    E, T = 12, 42
+    acts = np.random.RandomState(3).normal(0, 0.02, (T, E, 490)).astype(np.float32)
+    outs = []
+    for cat in (True, False):
+        eng = _engine(ds, E, None, cat=cat)
+        eng.seed(list(range(E)))
+        eng.reset()
+        outs.append([{k: v.copy() for k, v in eng.step(acts[t]).items()} for t in range(T)])
+        eng.close()
+    for a, b in zip(*outs):
+        np.testing.assert_allclose(a['obs'], b['obs'], rtol=2e-6, atol=1e-9)
+        assert np.array_equal(a['done'], b['done'])
+        assert np.array_equal(a['episode_len'], b['episode_len'])
+        assert np.array_equal(a['accuracy'], b['accuracy'])
 
 
 @pytest.mark.parametrize('lr_waves', [4, 8])
