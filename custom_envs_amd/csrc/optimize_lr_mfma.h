@@ -61,8 +61,33 @@ typedef double lr_d4 __attribute__((ext_vector_type(4)));
 #ifndef CE_LR_NOCLAMP
 #define CE_LR_NOCLAMP 1
 #endif
+//  CE_LR_WT       the outputs and state are stored write-through (sc1: an
+//                 agent-scope relaxed atomic store), so the launch ends with
+//                 less dirty L2 for the kernel boundary to write back
+#ifndef CE_LR_WT
+#define CE_LR_WT 0
+#endif
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
+
+// plain or write-through (CE_LR_WT) stores of 4- and 8-byte values
+template <typename T>
+__device__ __forceinline__ void lr_store(T *p, T v) {
+#if CE_LR_WT
+    if constexpr (sizeof(T) == 8) {
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned long long *)(p),
+                           __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (sizeof(T) == 4) {
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned *)(p),
+                           __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *p = v;
+    }
+#else
+    *p = v;
+#endif
+}
 constexpr int kLrMaxF = 16;
 // Waves per workgroup W (the row split) is a template parameter: 8 waves
 // (2 per SIMD, 2 tiles each) or 4 waves (1 per SIMD, 4 tiles per group,
@@ -505,10 +530,10 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     // episode length
 #pragma unroll
     for (int r = 0; r < PR; ++r)
-        if (prole[r] && OL == 0) a.obs[static_cast<unsigned>(e0 + pj[r]) * OS + pp[r]] = 0.0f;
+        if (prole[r] && OL == 0) lr_store(&a.obs[static_cast<unsigned>(e0 + pj[r]) * OS + pp[r]], 0.0f);
     if (srole) {
         if (a.done) a.done[es] = cur >= a.max_steps ? 1 : 0;
-        a.episode_len[es] = cur;
+        lr_store(&a.episode_len[es], cur);
     }
     // partials of this wave: s (features h + 4r of env c); -log of the
     // cross-entropy factors and the hits summed over the env's 4 lane groups
@@ -547,12 +572,12 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
         const double acc = div_rcp(ht, dB, rB);
         const double lnew = div_rcp(loss - lprev, dL, rL);
         const bool wipe = cur >= a.max_steps && a.auto_reset;
-        a.reward[es] = static_cast<float>(-loss);
-        a.objective[es] = static_cast<float>(loss);     // B == N: the same numbers
-        a.accuracy[es] = static_cast<float>(acc);
-        a.obs[es * OS + P - OL] = wipe ? 0.0f : static_cast<float>(lnew);
-        a.L[es] = wipe ? 0.0 : lnew;
-        a.step[es] = wipe ? 0 : cur;
+        lr_store(&a.reward[es], static_cast<float>(-loss));
+        lr_store(&a.objective[es], static_cast<float>(loss));   // B == N: the same numbers
+        lr_store(&a.accuracy[es], static_cast<float>(acc));
+        lr_store(&a.obs[es * OS + P - OL], wipe ? 0.0f : static_cast<float>(lnew));
+        lr_store(&a.L[es], wipe ? 0.0 : lnew);
+        lr_store(&a.step[es], wipe ? 0 : cur);
     }
     // per (env, parameter): W', G', obs, or the auto-reset's W0 / zeros
 #pragma unroll
@@ -566,10 +591,10 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
         for (int w = 0; w < kLrWaves; ++w) sf += red_s[w][f >> 2][pj[r] + 16 * (f & 3)];
         const double g = div_rcp((pp[r] & 1) ? sf : -sf, dB, rB);
         const double gnew = div_rcp(g, fabs(g_prev[r]) + 1.0, rG[r]);
-        a.obs[static_cast<unsigned>(e0 + pj[r]) * OS + P + 1 + pp[r] - OL] =
-            wipe ? 0.0f : static_cast<float>(gnew);
-        a.W[gi[r]] = wipe ? w_init[r] : wsh[pj[r]][pp[r]];
-        a.G[gi[r]] = wipe ? 0.0 : gnew;
+        lr_store(&a.obs[static_cast<unsigned>(e0 + pj[r]) * OS + P + 1 + pp[r] - OL],
+                 wipe ? 0.0f : static_cast<float>(gnew));
+        lr_store(&a.W[gi[r]], wipe ? w_init[r] : wsh[pj[r]][pp[r]]);
+        lr_store(&a.G[gi[r]], wipe ? 0.0 : gnew);
     }
     CE_STAMP(4);
 #ifdef CE_DIAG

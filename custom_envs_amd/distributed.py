@@ -178,11 +178,17 @@ class ShardedEnvs:
         self.derived = engine.derived_fields() if hasattr(engine, 'derived_fields') else {}
         self.layout = PackedLayout(engine.output_fields(), max(self.counts))
         device = device if device is not None else torch.device('cuda', torch.cuda.current_device())
-        self.buffers = [torch.zeros(self.layout.nbytes, dtype=torch.uint8, device=device)
-                        for _ in range(slots)]
-        self.outs = [self.layout.views(b, engine.num_envs) for b in self.buffers]
-        self.gathered = [torch.empty(world * self.layout.nbytes, dtype=torch.uint8, device=device)
+        # In place: the engine writes its outputs straight into this rank's
+        # slot of the gathered buffer, so the all-gather moves only the other
+        # ranks' records (NCCL/RCCL in-place form: send = recv + rank * count;
+        # at world 1 it has nothing to move)
+        nb = self.layout.nbytes
+        self.gathered = [torch.zeros(world * nb, dtype=torch.uint8, device=device)
                          if self.collective else None for _ in range(slots)]
+        self.buffers = [g[rank * nb:(rank + 1) * nb] if g is not None
+                        else torch.zeros(nb, dtype=torch.uint8, device=device)
+                        for g in self.gathered]
+        self.outs = [self.layout.views(b, engine.num_envs) for b in self.buffers]
 
     @property
     def buffer(self):

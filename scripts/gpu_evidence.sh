@@ -43,5 +43,11 @@ timeout -k 10 400 python bench.py --workload mnist --cpu-seconds 10 > $OUT/bench
 echo "bench mnist rc=$rc"; fatal $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_mnist -o run --output-format csv -- python3 bench.py --workload mnist --profile-only --steps 10 --warmup 2 > $OUT/prof_mnist.log 2>&1; rc=$?
 echo "rocprof mnist rc=$rc"; fatal $rc
-for w in multi mlp nn mnist; do python3 -c "import json; d=json.loads([l for l in open('$OUT/bench_$w.log') if l.startswith('{')][-1]); print('$w', '%.4g' % d['value'], d['ms_per_step'], (d.get('cpu_baseline') or {}).get('value'))"; done
+timeout -k 10 600 python bench.py --workload mlp --hidden 256,256 --batch-size 32 --envs 1024 --steps 10 --warmup 2 --cpu-seconds 10 > $OUT/bench_net.log 2>&1; rc=$?
+echo "bench net rc=$rc"; fatal $rc
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_net -o run --output-format csv -- python3 bench.py --workload mlp --hidden 256,256 --batch-size 32 --envs 1024 --profile-only --steps 5 --warmup 1 > $OUT/prof_net.log 2>&1; rc=$?
+echo "rocprof net rc=$rc"; fatal $rc
+timeout -k 10 300 python bench.py --force-gather --no-cpu-baseline --steps 2000 --warmup 200 > $OUT/bench_gather.log 2>&1; rc=$?
+echo "bench gather rc=$rc"; fatal $rc
+for w in multi mlp nn mnist net gather; do python3 -c "import json; d=json.loads([l for l in open('$OUT/bench_$w.log') if l.startswith('{')][-1]); print('$w', '%.4g' % d['value'], d['ms_per_step'], (d.get('cpu_baseline') or {}).get('value'))"; done
 echo ALL_OK

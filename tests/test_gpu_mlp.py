@@ -306,8 +306,10 @@ def _relu_ties(model, weights, X, rel=2e-6):
 def _net_check(features, targets, eng, hidden, batch_size, seeds, steps, scale=1e-3):
     """Tolerances as for config 3.  At a step whose minibatch has a relu tie
     (_relu_ties) the observation row is checked against the tie-free part:
-    at most 0.1 % of its entries may exceed the tolerance (one unit's
-    column of one layer), and the reward / objective checks stay exact."""
+    at most 0.5 % of its entries may exceed the tolerance (a flipped unit
+    moves one column of its layer's kernel gradient, 784 of 538,645 entries
+    at the default network, and the rows it feeds), and the reward /
+    objective checks stay exact."""
     refs = []
     for s in seeds:
         env = OracleEnv(features, targets, batch_size=batch_size, model='mlp', hidden=hidden)
@@ -339,7 +341,7 @@ def _net_check(features, targets, eng, hidden, batch_size, seeds, steps, scale=1
                 ties += 1
                 scale_r = max(np.abs(obs).max(), 1e-30)
                 bad = np.abs(out['obs'][i].astype(np.float64) - obs) > RTOL * scale_r
-                assert bad.mean() <= 1e-3, (i, t, int(bad.sum()))
+                assert bad.mean() <= 5e-3, (i, t, int(bad.sum()))
             else:
                 _row_close(out['obs'][i], obs, what='env %d step %d' % (i, t))
             assert _rel(out['reward'][i], reward) <= RTOL, (i, t)
