@@ -64,8 +64,9 @@ typedef double lr_d4 __attribute__((ext_vector_type(4)));
 //  CE_LR_WT       the outputs and state are stored write-through (sc1: an
 //                 agent-scope relaxed atomic store), so the launch ends with
 //                 less dirty L2 for the kernel boundary to write back
+//                 (rocprof average 6.29 -> 6.10 us per 4096-env launch)
 #ifndef CE_LR_WT
-#define CE_LR_WT 0
+#define CE_LR_WT 1
 #endif
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
