@@ -974,7 +974,8 @@ def net_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
     P = eng.act_dim
     train_f, info_f = net_flops(dims, args.batch_size, 1024)
     achieved = (train_f + info_f) * E / (kernel_ms * 1e-3) / 1e12
-    line = {'metric': METRIC_MLP.replace('784-64-10 MLP', '-'.join(map(str, dims)) + ' network')}
+    line = {'metric': METRIC_MLP.replace('784-64-10 MLP @4096 envs',
+                                         '%s network @%d envs' % ('-'.join(map(str, dims)), E))}
     line.update(_common(args, world, E, S, elapsed, shard))
     line.update({
         'dtype': 'f32',
