@@ -46,6 +46,24 @@
 
 namespace ce {
 
+// A store of a 4- or 8-byte value, write-through (sc1: an agent-scope relaxed
+// atomic store) when WT: the L2 line is written back as the store lands, so a
+// launch ends with little dirty L2 for the kernel boundary to write back
+// (MI355X_MICROARCH.md, kernel boundaries).  Other sizes store plainly.
+template <bool WT, typename T>
+__device__ __forceinline__ void wt_store(T *p, T v) {
+    if constexpr (WT && sizeof(T) == 8) {
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned long long *)(p),
+                           __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (WT && sizeof(T) == 4) {
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned *)(p),
+                           __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *p = v;
+    }
+}
+
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 16;

@@ -74,20 +74,7 @@ constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
 // plain or write-through (CE_LR_WT) stores of 4- and 8-byte values
 template <typename T>
 __device__ __forceinline__ void lr_store(T *p, T v) {
-#if CE_LR_WT
-    if constexpr (sizeof(T) == 8) {
-        __hip_atomic_store((__attribute__((address_space(1))) unsigned long long *)(p),
-                           __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    } else if constexpr (sizeof(T) == 4) {
-        __hip_atomic_store((__attribute__((address_space(1))) unsigned *)(p),
-                           __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        *p = v;
-    }
-#else
-    *p = v;
-#endif
+    wt_store<CE_LR_WT != 0>(p, v);
 }
 constexpr int kLrMaxF = 16;
 // Waves per workgroup W (the row split) is a template parameter: 8 waves
@@ -394,6 +381,24 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     // chains cover the f64 latency), 2 at 4 waves per SIMD (the other waves
     // cover it, and the 128-register budget has no room for 4)
     constexpr int QC = W >= 16 ? 2 : 4;
+    // per (row, env) after the exp: p_y, q, the loss factor, min |u|, hit
+    auto post = [&](double uq, double t, int y, double &qo) {
+#if CE_LR_RCP1
+        const double inv = rcp_newton1(1.0 + t);        // p_y
+#else
+        const double inv = rcp_unit(1.0 + t);           // p_y
+#endif
+        const bool valid = !PAD || y >= 0;
+        qo = valid ? t * inv : 0.0;
+        prod *= valid ? inv + 1e-16 : 1.0;
+        // min(umin, |u|) as one v_min_f64 with the abs modifier (fmin of an
+        // MFMA result gets a canonicalising v_max_f64 first)
+        {
+            const double au = valid ? uq : 1.0;
+            asm("v_min_f64 %0, %1, |%2|" : "=v"(umin) : "v"(umin), "v"(au));
+        }
+        hits += (valid && uq > 0.0) ? 1 : 0;
+    };
     auto softmax = [&](auto clamp_c, const lr_d4 &u, const int (&ys)[4], double (&qv)[4]) {
 #pragma unroll
         for (int q0 = 0; q0 < 4; q0 += QC) {
@@ -405,25 +410,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
             }
             exp_neg_q<QC>(tx);                          // t = e^-u
 #pragma unroll
-            for (int i = 0; i < QC; ++i) {
-                const int q = q0 + i;
-                const double uq = u[q];
-#if CE_LR_RCP1
-                const double inv = rcp_newton1(1.0 + tx[i]);   // p_y
-#else
-                const double inv = rcp_unit(1.0 + tx[i]);   // p_y
-#endif
-                const bool valid = !PAD || ys[q] >= 0;
-                qv[q] = valid ? tx[i] * inv : 0.0;
-                prod *= valid ? inv + 1e-16 : 1.0;
-                // min(umin, |u|) as one v_min_f64 with the abs modifier (fmin of
-                // an MFMA result gets a canonicalising v_max_f64 first)
-                {
-                    const double au = valid ? uq : 1.0;
-                    asm("v_min_f64 %0, %1, |%2|" : "=v"(umin) : "v"(umin), "v"(au));
-                }
-                hits += (valid && uq > 0.0) ? 1 : 0;
-            }
+            for (int i = 0; i < QC; ++i) post(u[q0 + i], tx[i], ys[q0 + i], qv[q0 + i]);
         }
     };
     auto forward = [&](const double (&xv)[NKF]) {
