@@ -66,12 +66,6 @@ constexpr int kNnPad = 4;          // LDS row padding (floats)
 constexpr int kNnChunk = 256;      // threads (and observation rows) per block of nn_agent_rows_kernel
 constexpr int kNnUpdPer = 4;       // agents per thread of nn_update_kernel
 constexpr int kNnPrefetch = 8;     // 8-float k-chunks of W in flight per lane
-// CE_NN_ROW_REWARD: the replicated reward / done rows (optvecenv.py:43-45)
-// are written by nn_agent_rows_kernel, thread = row, beside the observation
-// rows, instead of by a per-env loop in nn_finalize_kernel
-#ifndef CE_NN_ROW_REWARD
-#define CE_NN_ROW_REWARD 1
-#endif
 
 struct NnArgs {
     int E, N, F, K, L, B, nb, H, max_batches, auto_reset;
@@ -756,10 +750,6 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_rows_kernel(NnArgs a) {
         a.rw[slot * plane + eb + r] = ow;
         a.rg[slot * plane + eb + r] = og;
         if (sc.wipe) a.theta_n[eb + p] = a.theta0[eb + p];
-#if CE_NN_ROW_REWARD
-        a.reward[e * a.P + r] = static_cast<float>(sc.reward);
-        a.done[e * a.P + r] = sc.terminal ? 1 : 0;
-#endif
     }
     // ---- the block's rows: global floats [g0, g0 + n), staged at LDS
     // position (global index - g0) + off, off = the run's float phase within
@@ -872,14 +862,12 @@ __global__ __launch_bounds__(kNnChunk) void nn_finalize_kernel(NnArgs a) {
         a.cursor[e] = sc.wipe || wrap ? 0 : cur;
         comp[0] = (wrap ? 1 : 0) | (sc.wipe ? 2 : 0);
     }
-#if !CE_NN_ROW_REWARD
     // reward / done rows (replicated per agent, optvecenv.py:43-45)
     const float rw = static_cast<float>(sc.reward);
     for (int r = tid; r < P; r += kNnChunk) {
         a.reward[e * P + r] = rw;
         a.done[e * P + r] = sc.terminal ? 1 : 0;
     }
-#endif
     __syncthreads();
     const int c = comp[0];
     if (c) {

@@ -30,13 +30,42 @@ int dev_alloc(T **p, size_t count) {
 }
 
 // W' = W - a over every env's parameters (optimize.py:74-75); the step
-// counter advances (baseenvironment.py:30-41: current_step += 1 first)
+// counter advances (baseenvironment.py:30-41: current_step += 1 first).
+// 16-byte accesses when both arrays allow them (W always does; an action
+// block of a ce_step_many stride may sit at 8 bytes), so each thread keeps
+// 32 bytes of loads in flight
 __global__ __launch_bounds__(kNetBlock) void net_update_kernel(float *W, const float *act,
                                                              size_t n, int32_t *step, int E) {
     const size_t i0 = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x;
     const size_t stride = static_cast<size_t>(gridDim.x) * kNetBlock;
-    for (size_t i = i0; i < n; i += stride) W[i] -= act[i];
     if (i0 < static_cast<size_t>(E)) step[i0] += 1;
+    if (((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(act)) & 15) == 0) {
+        float4 *w4 = reinterpret_cast<float4 *>(W);
+        const float4 *a4 = reinterpret_cast<const float4 *>(act);
+        const size_t n4 = n >> 2;
+        for (size_t i = i0; i < n4; i += stride) {
+            float4 w = w4[i];
+            const float4 v = a4[i];
+            w.x -= v.x;
+            w.y -= v.y;
+            w.z -= v.z;
+            w.w -= v.w;
+            w4[i] = w;
+        }
+        for (size_t i = 4 * n4 + i0; i < n; i += stride) W[i] -= act[i];
+    } else {
+        float2 *w2 = reinterpret_cast<float2 *>(W);
+        const float2 *a2 = reinterpret_cast<const float2 *>(act);
+        const size_t n2 = n >> 1;
+        for (size_t i = i0; i < n2; i += stride) {
+            float2 w = w2[i];
+            const float2 v = a2[i];
+            w.x -= v.x;
+            w.y -= v.y;
+            w2[i] = w;
+        }
+        for (size_t i = 2 * n2 + i0; i < n; i += stride) W[i] -= act[i];
+    }
 }
 
 // sequence[0]: rows order[0 .. B) of each env's current order
@@ -56,7 +85,9 @@ __global__ __launch_bounds__(kNetBlock) void net_gather_kernel(NetArgs a, float 
     }
 }
 
-// H[e] (R x d) += b_l[e]; relu (the hidden Dense layers' activation)
+// H[e] (R x d) += b_l[e]; relu (the hidden Dense layers' activation).  With
+// d % 4 == 0 four units per thread (16-byte H accesses; the bias slab sits at
+// an 8-byte boundary: P and the layer offsets are even)
 __global__ __launch_bounds__(kNetBlock) void net_bias_act_kernel(float *H, int R, int d,
                                                                const float *W, int64_t P,
                                                                int64_t offb) {
@@ -64,8 +95,25 @@ __global__ __launch_bounds__(kNetBlock) void net_bias_act_kernel(float *H, int R
     const size_t n = static_cast<size_t>(R) * d;
     float *h = H + static_cast<size_t>(e) * n;
     const float *b = W + static_cast<size_t>(e) * P + offb;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; i < n;
-         i += static_cast<size_t>(gridDim.x) * kNetBlock) {
+    const size_t i0 = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kNetBlock;
+    if ((d & 3) == 0 && ((reinterpret_cast<uintptr_t>(b) & 7) == 0)) {
+        float4 *h4 = reinterpret_cast<float4 *>(h);
+        const float2 *b2 = reinterpret_cast<const float2 *>(b);
+        const int d4 = d >> 2;
+        for (size_t i = i0; i < n >> 2; i += stride) {
+            const int j = static_cast<int>(i % d4);
+            const float2 lo = b2[2 * j], hi = b2[2 * j + 1];
+            float4 v = h4[i];
+            v.x = fmaxf(v.x + lo.x, 0.0f);
+            v.y = fmaxf(v.y + lo.y, 0.0f);
+            v.z = fmaxf(v.z + hi.x, 0.0f);
+            v.w = fmaxf(v.w + hi.y, 0.0f);
+            h4[i] = v;
+        }
+        return;
+    }
+    for (size_t i = i0; i < n; i += stride) {
         const int j = static_cast<int>(i % d);
         h[i] = fmaxf(h[i] + b[j], 0.0f);
     }
@@ -171,6 +219,10 @@ __global__ __launch_bounds__(kNetBlock) void net_relu_back_kernel(float *dH, con
 // float64), obs = [0 (P) | L' (written per env) | G' (P)]; the auto-reset
 // (utils_venv.py:31) of an env whose step ends its episode: W <- W0, G <- 0,
 // obs <- 0 (the reset observation).  step[e] already holds current_step.
+// With P even (every shape whose hidden widths are even), two parameters per
+// thread: the env's grad / W / W0 slabs then sit at 8-byte and its G slab at
+// 16-byte boundaries (float2 / double2 accesses); the observation rows
+// (2P + 1 floats) take scalar stores.
 __global__ __launch_bounds__(kNetBlock) void net_epilogue_kernel(NetArgs a, const float *grad) {
     const int e = blockIdx.y;
     const int cur = a.step[e];
@@ -178,11 +230,33 @@ __global__ __launch_bounds__(kNetBlock) void net_epilogue_kernel(NetArgs a, cons
     const size_t P = a.P, base = static_cast<size_t>(e) * P;
     float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
     const float fb = static_cast<float>(a.B);
-    for (size_t p = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; p < P;
-         p += static_cast<size_t>(gridDim.x) * kNetBlock) {
+    const size_t t0 = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kNetBlock;
+    if ((P & 1) == 0) {
+        const float2 *g2 = reinterpret_cast<const float2 *>(grad + base);
+        double2 *G2 = reinterpret_cast<double2 *>(a.G + base);
+        for (size_t q = t0; q < P / 2; q += stride) {
+            const float2 gv = g2[q];
+            const double2 Gv = G2[q];
+            const float ga = gv.x / fb, gb = gv.y / fb;
+            const double na = static_cast<double>(ga) / (fabs(Gv.x) + 1.0);
+            const double nb = static_cast<double>(gb) / (fabs(Gv.y) + 1.0);
+            const size_t p = 2 * q;
+            obs[p] = 0.0f;                                // wght_hist is identically 0
+            obs[p + 1] = 0.0f;
+            obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(na);
+            obs[P + 2 + p] = wipe ? 0.0f : static_cast<float>(nb);
+            G2[q] = wipe ? double2{0.0, 0.0} : double2{na, nb};
+            if (wipe)
+                reinterpret_cast<float2 *>(a.W + base)[q] =
+                    reinterpret_cast<const float2 *>(a.W0 + base)[q];
+        }
+        return;
+    }
+    for (size_t p = t0; p < P; p += stride) {
         const float g = grad[base + p] / fb;
         const double gn = static_cast<double>(g) / (fabs(a.G[base + p]) + 1.0);
-        obs[p] = 0.0f;                                    // wght_hist is identically 0
+        obs[p] = 0.0f;
         obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(gn);
         a.G[base + p] = wipe ? 0.0 : gn;
         if (wipe) a.W[base + p] = a.W0[base + p];
@@ -474,7 +548,7 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         hipLaunchKernelGGL(net_softmax_kernel, dim3(E), dim3(kNetBlock), 0, s, p->inf_out, N, K, a.W,
                            P, p->offb[nl - 1], a.label, int64_t(0), false, p->inf_loss, p->inf_hits);
     }
-    hipLaunchKernelGGL(net_epilogue_kernel, dim3(blocks_for(static_cast<size_t>(P), 1024), E),
+    hipLaunchKernelGGL(net_epilogue_kernel, dim3(blocks_for(static_cast<size_t>(P + 1) / 2, 1024), E),
                        dim3(kNetBlock), 0, s, a, p->grad);
     hipLaunchKernelGGL(net_finish_kernel, dim3(E), dim3(kNetBlock), 0, s, a, p->mb_loss, p->mb_hits,
                        p->inf_loss, p->inf_hits);

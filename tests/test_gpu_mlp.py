@@ -365,11 +365,14 @@ def test_default_network_256x256(batch_size):
         eng.close()
 
 
-@pytest.mark.parametrize('hidden,batch_size', [((96, 32, 48), 20), ((40,), None), ((64,), 32)])
+@pytest.mark.parametrize('hidden,batch_size', [((96, 32, 48), 20), ((40,), None), ((64,), 32),
+                                               ((33, 7), 24)])
 def test_network_shapes(hidden, batch_size, monkeypatch):
     """Three hidden layers, one layer with the full batch (B = N: the info pass
-    reuses the minibatch numbers), and config 3's shape forced onto the
-    layered path (CE_MLP_NET=1) -- 5 envs, one mid-episode reset crossed."""
+    reuses the minibatch numbers), config 3's shape forced onto the layered
+    path (CE_MLP_NET=1), and odd widths (P = 26,223 is odd: the epilogue's
+    scalar path, bias slabs off 8-byte boundaries) -- 5 envs, one
+    mid-episode reset crossed."""
     from oracle.gen_golden import mlp_dataset
     features, targets = mlp_dataset()
     force = hidden == (64,)
