@@ -248,6 +248,24 @@ class OptimizeEngine:
         check(self._lib.ce_step_many(self._h, int(k), actions.data_ptr(), stride,
                                      ctypes.byref(o)), 'ce_step_many')
 
+    def many_runner(self, k, actions, out, per_step_actions=True):
+        """step_many_device bound once: the tensors are checked and the
+        argument struct built here, and the returned callable issues the k
+        steps with one foreign call (a training loop replaying fixed device
+        buffers pays no per-call Python validation).  The callable holds
+        references to `actions` and `out`."""
+        self._check_device_tensors(actions, out, k if per_step_actions else 1)
+        stride = self.num_envs * self.act_dim if per_step_actions else 0
+        o = self._outputs(out)
+        fn, h, ap, ref, kk = self._lib.ce_step_many, self._h, actions.data_ptr(), ctypes.byref(o), int(k)
+
+        def run():
+            rc = fn(h, kk, ap, stride, ref)
+            if rc:
+                check(rc, 'ce_step_many')
+        run.keep = (actions, out, o)
+        return run
+
     def prepare_many_device(self, k, actions, out, per_step_actions=True):
         """Instantiate (and upload) the k-step hipGraph without running it."""
         self._check_device_tensors(actions, out, k if per_step_actions else 1)

@@ -208,10 +208,11 @@ def test_single_env_api_matches_oracle(lr_dataset):
     env.close()
 
 
-@pytest.mark.parametrize('many_direct', ['32', '0'])
-def test_device_path_matches_host_path(lr_dataset, many_direct, monkeypatch):
-    """ce_step_many as plain launches (k <= CE_MANY_DIRECT, default 32) and
-    as a replayed hipGraph (CE_MANY_DIRECT=0) give the host path's bits."""
+@pytest.mark.parametrize('many_direct,bound', [('32', False), ('0', False), ('32', True)])
+def test_device_path_matches_host_path(lr_dataset, many_direct, bound, monkeypatch):
+    """ce_step_many as plain launches (k <= CE_MANY_DIRECT, default 32), as a
+    replayed hipGraph (CE_MANY_DIRECT=0) and through the pre-bound
+    many_runner give the host path's bits."""
     import torch
     monkeypatch.setenv('CE_MANY_DIRECT', many_direct)
     E, P, K = 512, 20, 12
@@ -229,7 +230,12 @@ def test_device_path_matches_host_path(lr_dataset, many_direct, monkeypatch):
         out = dev.alloc_device_outputs()
         dact = torch.from_numpy(acts).cuda()
         dev.reset_device(out)
-        dev.step_many_device(K, dact, out)
+        if bound:
+            run = dev.many_runner(K // 2, dact[:K // 2], out)
+            run()
+            dev.many_runner(K - K // 2, dact[K // 2:], out)()
+        else:
+            dev.step_many_device(K, dact, out)
     torch.cuda.synchronize()
     assert np.array_equal(out['obs'].cpu().numpy(), ref['obs'])
     assert np.array_equal(out['reward'].cpu().numpy(), ref['reward'])
