@@ -477,6 +477,7 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         const char *lrm = std::getenv("CE_LR_MFMA");
         lr_path = !generic && !(lrm && lrm[0] == '0') && !std::getenv("CE_PAIR_U") &&
                   cfg->precision == CE_F64 && cfg->batch_size == cfg->n_rows &&
+                  cfg->num_envs < (1 << 24) &&      // its packed E | F << 24 argument
                   ce::lr_shape_ok(cfg->n_features, cfg->n_classes);
         if (!generic && !lr_path)
             kern = find_kernel(cfg->precision, cfg->n_features, cfg->n_classes);

@@ -188,8 +188,17 @@ __device__ __forceinline__ int fold_env_lanes(int v) {
     return static_cast<int>(x + y);
 }
 
+// Everything the prologue's load addresses need -- the weights, actions,
+// data-set image, G, step and L arrays, E | F << 24 and N -- comes as leading
+// scalar arguments as well as in `a`: built with
+// -amdgpu-kernarg-preload-count=14 (build.py) they arrive in SGPRs at wave
+// launch, so every state and tile load issues without waiting for the
+// kernel-argument load (~530 cycles)
 template <int NKF, int MODE, int W>
-__global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(StepArgs<double> a) {
+__global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
+    double *Wp, const float *actp, const unsigned char *datap, double *Gp, int32_t *stepp, double *Lp,
+    unsigned efp, int Np, StepArgs<double> a) {
+    const int Ep = static_cast<int>(efp & 0xffffffu), Fp = static_cast<int>(efp >> 24);
     constexpr int kLrWaves = W;
     constexpr int kLrBlock = LrShape<W>::kBlock;
     constexpr int P_MAX = 2 * kLrMaxF;
@@ -211,23 +220,23 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, h = lane >> 4;
-    const int F = a.F, P = 2 * F, N = a.N, B = a.B;
+    const int F = Fp, P = 2 * F, N = Np, B = a.B;
     // observation rows: obs_stride floats per env from entry obs_lo on (the
     // compact form, obs_lo = P, leaves out the identically-zero weight block)
     const int OS = a.obs_stride, OL = a.obs_lo;
     const int e0 = blockIdx.x * kLrEnvs;
     const int e = e0 + c;                               // this lane's env (columns)
-    const bool env_ok = e < a.E;
+    const bool env_ok = e < Ep;
     // 32-bit element offsets throughout: every load / store is a uniform
     // base (SGPRs) + a VGPR offset, no 64-bit address arithmetic
     const unsigned pbase = static_cast<unsigned>(env_ok ? e : 0) * P;
-    const double *img = reinterpret_cast<const double *>(a.data);
+    const double *img = reinterpret_cast<const double *>(datap);
     const int ntiles = (N + 15) / 16;
 
-    // ---- every state load of the step issued before any is used, ahead of
-    // the row tiles' loads (one memory round trip; waiting for the state
-    // does not wait for the tiles):
+    // ---- every load of the step issued before any is used (one memory
+    // round trip), in the order they are needed (vmcnt retires in order):
     //  - W and the action of features 4k + h of env c (forward B operand);
+    //  - the first group's row tiles (forward A operands);
     //  - role "parameter" (index i = j P + p < 16 P, i = tid + r kLrBlock):
     //    G and W0 of parameter p of env e0 + j and that env's step counter;
     //  - role "scalar" (the last 16 threads, one per env of the group): L
@@ -242,38 +251,12 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     for (int k = 0; k < NKF; ++k) {
         const int f = 4 * k + h;
         const unsigned i0 = pbase + (f < F ? 2 * f : 0);
-        wv[k] = *reinterpret_cast<const double2 *>(a.W + i0);   // 16-B aligned: P even
-        av[k] = *reinterpret_cast<const float2 *>(a.act + i0);  // 8-B aligned
+        wv[k] = *reinterpret_cast<const double2 *>(Wp + i0);   // 16-B aligned: P even
+        av[k] = *reinterpret_cast<const float2 *>(actp + i0);  // 8-B aligned
 #if CE_LR_NOCLAMP
         xm[k] = colmax[f];
 #endif
     }
-    const int np_ = kLrEnvs * P;
-    int pj[PR], pp[PR], step_p[PR];
-    bool prole[PR];
-    unsigned gi[PR];
-    double g_prev[PR], w_init[PR];
-#pragma unroll
-    for (int r = 0; r < PR; ++r) {
-        const int i = tid + r * kLrBlock;
-        pj[r] = (i * a.p_mul) >> 16;                    // i / P, exact for i < 2^9
-        pp[r] = i - pj[r] * P;
-        prole[r] = i < np_ && e0 + pj[r] < a.E;
-        gi[r] = static_cast<unsigned>(prole[r] ? e0 + pj[r] : 0) * P + (prole[r] ? pp[r] : 0);
-        g_prev[r] = a.G[gi[r]];
-#if CE_LR_W0_LAZY
-        w_init[r] = 0.0;                                // loaded below, wiping envs only
-#else
-        w_init[r] = a.W0[gi[r]];
-#endif
-        step_p[r] = a.step[prole[r] ? e0 + pj[r] : 0];
-    }
-    const int sj = tid - (kLrBlock - kLrEnvs);
-    const bool srole = sj >= 0 && e0 + sj < a.E;
-    const unsigned es = srole ? e0 + sj : 0;
-    const double lprev = a.L[es];
-    const int step_prev = a.step[es];
-
     // the wave's row tiles, each group's forward operands loaded a group ahead
     constexpr bool PAD = MODE == 0;
     // forward A of tile t: X~[16t + c][4k + h]; labels of rows 16t + h + 4q
@@ -296,7 +279,36 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
 #pragma unroll
         for (int i = 0; i < NT; ++i) operands(t + i * kLrWaves, xf[i], yl[i], PAD && i == 0);
     };
+    // the first group's tile loads right behind W and the action: the
+    // G / step / L loads below are the epilogue's and may wait
     load_group(wave < ntiles ? wave : 0);              // unconditional: no merge-point vmcnt(0)
+    const int np_ = kLrEnvs * P;
+    const int pmul = (65536 + P - 1) / P;              // a.p_mul, formed here (uniform)
+    int pj[PR], pp[PR], step_p[PR];
+    bool prole[PR];
+    unsigned gi[PR];
+    double g_prev[PR], w_init[PR];
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+        const int i = tid + r * kLrBlock;
+        pj[r] = (i * pmul) >> 16;                     // i / P, exact for i < 2^9
+        pp[r] = i - pj[r] * P;
+        prole[r] = i < np_ && e0 + pj[r] < Ep;
+        gi[r] = static_cast<unsigned>(prole[r] ? e0 + pj[r] : 0) * P + (prole[r] ? pp[r] : 0);
+        g_prev[r] = Gp[gi[r]];
+#if CE_LR_W0_LAZY
+        w_init[r] = 0.0;                                // loaded below, wiping envs only
+#else
+        w_init[r] = a.W0[gi[r]];
+#endif
+        step_p[r] = stepp[prole[r] ? e0 + pj[r] : 0];
+    }
+    const int sj = tid - (kLrBlock - kLrEnvs);
+    const bool srole = sj >= 0 && e0 + sj < Ep;
+    const unsigned es = srole ? e0 + sj : 0;
+    const double lprev = Lp[es];
+    const int step_prev = stepp[es];
+
 
     // ---- W' = W - a (optimize.py:74-75); forward B operand: the margin
     // w'_f0 - w'_f1 of feature 4k + h for env c
@@ -564,8 +576,8 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
         lr_store(&a.objective[es], static_cast<float>(loss));   // B == N: the same numbers
         lr_store(&a.accuracy[es], static_cast<float>(acc));
         lr_store(&a.obs[es * OS + P - OL], wipe ? 0.0f : static_cast<float>(lnew));
-        lr_store(&a.L[es], wipe ? 0.0 : lnew);
-        lr_store(&a.step[es], wipe ? 0 : cur);
+        lr_store(&Lp[es], wipe ? 0.0 : lnew);
+        lr_store(&stepp[es], wipe ? 0 : cur);
     }
     // per (env, parameter): W', G', obs, or the auto-reset's W0 / zeros
 #pragma unroll
@@ -581,8 +593,8 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
         const double gnew = div_rcp(g, fabs(g_prev[r]) + 1.0, rG[r]);
         lr_store(&a.obs[static_cast<unsigned>(e0 + pj[r]) * OS + P + 1 + pp[r] - OL],
                  wipe ? 0.0f : static_cast<float>(gnew));
-        lr_store(&a.W[gi[r]], wipe ? w_init[r] : wsh[pj[r]][pp[r]]);
-        lr_store(&a.G[gi[r]], wipe ? 0.0 : gnew);
+        lr_store(&Wp[gi[r]], wipe ? w_init[r] : wsh[pj[r]][pp[r]]);
+        lr_store(&Gp[gi[r]], wipe ? 0.0 : gnew);
     }
     CE_STAMP(4);
 #ifdef CE_DIAG
@@ -590,7 +602,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(St
     CE_STAMP(5);
     stamps[7] = __builtin_amdgcn_s_memrealtime();
     const int row = blockIdx.x * kLrWaves + wave;
-    if (row < a.E && lane < kStamps) a.diag[static_cast<size_t>(row) * kStamps + lane] = stamps[lane];
+    if (row < Ep && lane < kStamps) a.diag[static_cast<size_t>(row) * kStamps + lane] = stamps[lane];
 #endif
 }
 

@@ -109,26 +109,35 @@ void lr_choice(int E, int N, int lr_waves, int mode_cap, int *w_out, int *mode_o
     *mode_out = mode;
 }
 
+// E | F << 24: the two-class kernel's preloaded size word (E < 2^24, F <= 16)
+unsigned lr_ef(const StepArgs<double> &a) {
+    return static_cast<unsigned>(a.E) | (static_cast<unsigned>(a.F) << 24);
+}
+
 template <int NKF, int W>
 void launch_lr_w(const StepArgs<double> &a, int mode, hipStream_t stream) {
     const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
     const dim3 block(LrShape<W>::kBlock);
     if constexpr (W <= 4) {
         if (mode == 3) {
-            hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 3, W>), dim3(grid), block, 0, stream, a);
+            hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 3, W>), dim3(grid), block, 0, stream, a.W, a.act,
+                               a.data, a.G, a.step, a.L, lr_ef(a), a.N, a);
             return;
         }
     }
     if constexpr (W <= 8) {   // 16 waves take their tiles one at a time (128 registers)
         if (mode == 2) {
-            hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 2, W>), dim3(grid), block, 0, stream, a);
+            hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 2, W>), dim3(grid), block, 0, stream, a.W, a.act,
+                               a.data, a.G, a.step, a.L, lr_ef(a), a.N, a);
             return;
         }
     }
     if (mode >= 1)
-        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 1, W>), dim3(grid), block, 0, stream, a);
+        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 1, W>), dim3(grid), block, 0, stream, a.W, a.act,
+                               a.data, a.G, a.step, a.L, lr_ef(a), a.N, a);
     else
-        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 0, W>), dim3(grid), block, 0, stream, a);
+        hipLaunchKernelGGL((optimize_lr_mfma_kernel<NKF, 0, W>), dim3(grid), block, 0, stream, a.W, a.act,
+                               a.data, a.G, a.step, a.L, lr_ef(a), a.N, a);
 }
 
 template <int NKF>
