@@ -1005,9 +1005,10 @@ def net_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
         'roofline': {
             'bound': 'mfma', 'achieved': achieved, 'peak': MFMA_F32_PEAK_TFLOPS,
             'unit': 'TFLOP/s', 'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': None,
-            'kernel': 'one step = %s: strided-batched rocBLAS sgemm per layer (forward, dW, '
-                      'dH, info forward) + net_update/gather/bias_act/softmax/colsum/relu_back/'
-                      'epilogue/finish kernels' % eng.step_kernel,
+            'kernel': 'one step = %s: strided-batched f32 GEMMs per layer, bias by a ones '
+                      'column (hidden forwards on hipBLASLt with the relu epilogue when :lt; '
+                      'dW/db, dH, output layer on rocBLAS) + net_update/gather/softmax/'
+                      'relu_back/epilogue/finish kernels' % eng.step_kernel,
             'flops_per_env_step': train_f + info_f, 'info_flops_per_env_step': info_f,
             'step_ms_median': kernel_ms, 'step_ms_mean': kernel_ms_mean,
         },

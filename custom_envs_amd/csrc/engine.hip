@@ -621,7 +621,10 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
             if ((rc = ce::net_create(&e->net, a, cfg->device)) != CE_OK) return bail(rc);
             std::string name = "net<";
             for (size_t i = 0; i < dims.size(); ++i) name += (i ? "," : "") + std::to_string(dims[i]);
-            e->kernel_name = name + ">";
+            // ":lt": every hidden-layer forward runs on hipBLASLt with the
+            // relu epilogue; ":relu": rocBLAS plus a relu pass (CE_NET_LT=0,
+            // or a shape without a hipBLASLt solution)
+            e->kernel_name = name + (ce::net_forward_lt(e->net) ? ">:lt" : ">:relu");
         }
     }
 #undef CE_TRY

@@ -9,16 +9,19 @@
 //   net_update_kernel   W' = W - a (optimize.py:74-75), step += 1, and the
 //                       minibatch rows of each env gathered through its
 //                       row order (sequence[0], B < N)
-//   forward             per layer one strided-batched rocBLAS sgemm over the
-//                       E envs (H_l = H_{l-1} W_l), then net_bias_act_kernel
-//                       (+ b_l, relu) -- the dense products are plain library
-//                       GEMMs; the per-env parameter slabs are the GEMM batch
+//   forward             per layer one strided-batched f32 GEMM over the E envs,
+//                       H_l = relu([H_{l-1} | 1] [W_l; b_l]): the bias by the
+//                       ones column of the augmented input, the relu as the
+//                       hipBLASLt epilogue (rocBLAS + a relu pass where no
+//                       hipBLASLt solution fits, or CE_NET_LT=0) -- the dense
+//                       products are plain library GEMMs; the per-env
+//                       parameter slabs are the GEMM batch
 //   net_softmax_kernel  softmax, -log(p_y + 1e-16), argmax hit per row, the
 //                       per-env loss / hit sums, dZ = P - Y (utils_math.py:
 //                       25-34,51-63)
-//   backward            dW_l = H_{l-1}^T dZ_l straight into the env's gradient
-//                       slab, db_l = column sums (net_colsum_kernel),
-//                       dH_{l-1} = dZ_l W_l^T, relu' (net_relu_back_kernel)
+//   backward            [dW_l; db_l] = [H_{l-1} | 1]^T dZ_l straight into the
+//                       env's gradient slab (one GEMM), dH_{l-1} = dZ_l W_l^T,
+//                       relu' (net_relu_back_kernel)
 //   info (B < N)        the full-data forward for info['objective'] /
 //                       ['accuracy'] (optimize.py:94-97); B == N reuses the
 //                       minibatch numbers, as the reference computes the same
@@ -63,13 +66,16 @@ struct NetArgs {
 
 struct NetPlan;
 
-// Work buffers and the rocBLAS handle for E envs of this shape.
+// Work buffers, the rocBLAS / hipBLASLt handles and the forward GEMMs'
+// hipBLASLt algorithms for E envs of this shape.
 int net_create(NetPlan **out, const NetArgs &shape, int device);
 void net_destroy(NetPlan *plan);
 // Stream-ordered launches of one step / one reset (no host synchronisation:
 // capturable into a hipGraph).
 int net_step(NetPlan *plan, const NetArgs &a, hipStream_t stream);
 int net_reset(NetPlan *plan, const NetArgs &a, hipStream_t stream);
+// True when every hidden-layer forward has a hipBLASLt relu-epilogue algorithm.
+bool net_forward_lt(const NetPlan *plan);
 // Flat parameter count of the network.
 int64_t net_params(int F, int K, int n_hidden, const int *hidden);
 

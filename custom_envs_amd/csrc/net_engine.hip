@@ -1,16 +1,26 @@
 // Optimize-v0 over a general OptimizeNN network (net_engine.h has the step's
 // launch sequence).  The dense products of every layer are plain GEMMs over
-// the envs' parameter slabs -- strided-batched rocBLAS sgemm, batch = envs,
-// the dataset operand shared (stride 0) -- and everything around them is
-// hand-written: the update and the minibatch gather, bias + relu, the
-// softmax / cross-entropy / argmax with its per-env reductions, the bias
-// gradients, relu', and the float64 epilogue.
+// the envs' parameter slabs -- strided-batched f32 GEMMs, batch = envs, the
+// dataset operand shared (stride 0) -- and everything around them is
+// hand-written: the update and the minibatch gather, the softmax /
+// cross-entropy / argmax with its per-env reductions, relu', and the float64
+// epilogue.
+//
+// Bias by augmentation: an env's flat slab [W_l (d_in x d_out) | b_l
+// (d_out)] IS the row-major (d_in + 1) x d_out matrix [W_l; b_l], so every
+// layer input carries a ones column (activation rows [h_0 .. h_{d-1} | 1 |
+// 0 0 0], row stride ld_aug(d)) and one GEMM with K = d_in + 1 gives
+// H W + b; its transpose product H_aug^T dZ gives [dW; db] straight into the
+// gradient slab.  The hidden layers' relu is the GEMM's epilogue (hipBLASLt
+// HIPBLASLT_EPILOGUE_RELU), so no activation makes an extra HBM pass.
 #include "net_engine.h"
 
+#include <hipblaslt/hipblaslt.h>
 #include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -20,6 +30,10 @@ namespace {
 
 constexpr int kNetBlock = 256;
 constexpr int kNetMaxK = 32;
+
+// Row stride of an augmented activation buffer: d values, the ones column,
+// rounded up to 16 bytes
+__host__ __device__ constexpr int ld_aug(int d) { return (d + 1 + 3) & ~3; }
 
 template <typename T>
 int dev_alloc(T **p, size_t count) {
@@ -32,8 +46,9 @@ int dev_alloc(T **p, size_t count) {
 // W' = W - a over every env's parameters (optimize.py:74-75); the step
 // counter advances (baseenvironment.py:30-41: current_step += 1 first).
 // 16-byte accesses when both arrays allow them (W always does; an action
-// block of a ce_step_many stride may sit at 8 bytes), so each thread keeps
-// 32 bytes of loads in flight
+// block of a ce_step_many stride may sit at 8 bytes), kNetUpd of them per
+// array in flight per thread before any store
+constexpr int kNetUpd = 4;
 __global__ __launch_bounds__(kNetBlock) void net_update_kernel(float *W, const float *act,
                                                              size_t n, int32_t *step, int E) {
     const size_t i0 = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x;
@@ -43,14 +58,21 @@ __global__ __launch_bounds__(kNetBlock) void net_update_kernel(float *W, const f
         float4 *w4 = reinterpret_cast<float4 *>(W);
         const float4 *a4 = reinterpret_cast<const float4 *>(act);
         const size_t n4 = n >> 2;
-        for (size_t i = i0; i < n4; i += stride) {
-            float4 w = w4[i];
-            const float4 v = a4[i];
-            w.x -= v.x;
-            w.y -= v.y;
-            w.z -= v.z;
-            w.w -= v.w;
-            w4[i] = w;
+        for (size_t i = i0; i < n4; i += kNetUpd * stride) {
+            float4 w[kNetUpd], v[kNetUpd];
+#pragma unroll
+            for (int q = 0; q < kNetUpd; ++q) {
+                const size_t j = i + q * stride;
+                const size_t jc = j < n4 ? j : i;                 // in range: i < n4
+                w[q] = w4[jc];
+                v[q] = a4[jc];
+            }
+#pragma unroll
+            for (int q = 0; q < kNetUpd; ++q) {
+                const size_t j = i + q * stride;
+                if (j < n4) w4[j] = float4{w[q].x - v[q].x, w[q].y - v[q].y, w[q].z - v[q].z,
+                                           w[q].w - v[q].w};
+            }
         }
         for (size_t i = 4 * n4 + i0; i < n; i += stride) W[i] -= act[i];
     } else {
@@ -75,69 +97,54 @@ __global__ __launch_bounds__(kNetBlock) void net_gather_kernel(NetArgs a, float 
     const int sel = a.order_sel[e];
     const int32_t *order = a.order + (static_cast<size_t>(sel) * a.E + e) * a.N;
     const size_t n = static_cast<size_t>(a.B) * a.F;
-    float *dst = xb + static_cast<size_t>(e) * n;
+    const int ldx = ld_aug(a.F);                        // the ones column is never rewritten
+    float *dst = xb + static_cast<size_t>(e) * a.B * ldx;
     for (size_t i = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; i < n;
          i += static_cast<size_t>(gridDim.x) * kNetBlock) {
         const int r = static_cast<int>(i / a.F), f = static_cast<int>(i - static_cast<size_t>(r) * a.F);
         const int row = order[r];
-        dst[i] = a.X[static_cast<size_t>(row) * a.F + f];
+        dst[static_cast<size_t>(r) * ldx + f] = a.X[static_cast<size_t>(row) * a.F + f];
         if (f == 0) yb[static_cast<size_t>(e) * a.B + r] = a.label[row];
     }
 }
 
-// H[e] (R x d) += b_l[e]; relu (the hidden Dense layers' activation).  With
-// d % 4 == 0 four units per thread (16-byte H accesses; the bias slab sits at
-// an 8-byte boundary: P and the layer offsets are even)
-__global__ __launch_bounds__(kNetBlock) void net_bias_act_kernel(float *H, int R, int d,
-                                                               const float *W, int64_t P,
-                                                               int64_t offb) {
-    const int e = blockIdx.y;
-    const size_t n = static_cast<size_t>(R) * d;
-    float *h = H + static_cast<size_t>(e) * n;
-    const float *b = W + static_cast<size_t>(e) * P + offb;
-    const size_t i0 = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x;
-    const size_t stride = static_cast<size_t>(gridDim.x) * kNetBlock;
-    if ((d & 3) == 0 && ((reinterpret_cast<uintptr_t>(b) & 7) == 0)) {
-        float4 *h4 = reinterpret_cast<float4 *>(h);
-        const float2 *b2 = reinterpret_cast<const float2 *>(b);
-        const int d4 = d >> 2;
-        for (size_t i = i0; i < n >> 2; i += stride) {
-            const int j = static_cast<int>(i % d4);
-            const float2 lo = b2[2 * j], hi = b2[2 * j + 1];
-            float4 v = h4[i];
-            v.x = fmaxf(v.x + lo.x, 0.0f);
-            v.y = fmaxf(v.y + lo.y, 0.0f);
-            v.z = fmaxf(v.z + hi.x, 0.0f);
-            v.w = fmaxf(v.w + hi.y, 0.0f);
-            h4[i] = v;
-        }
-        return;
-    }
-    for (size_t i = i0; i < n; i += stride) {
-        const int j = static_cast<int>(i % d);
-        h[i] = fmaxf(h[i] + b[j], 0.0f);
+// rows x ld buffer: column `col` = 1, the columns after it = 0 (the ones
+// column of the bias augmentation, written once: no GEMM writes past d);
+// with src, columns < col are copied from the src rows (stride col)
+__global__ __launch_bounds__(kNetBlock) void net_aug_kernel(float *buf, size_t rows, int ld, int col,
+                                                          const float *src) {
+    const size_t n = rows * ld;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; i < n;
+         i += static_cast<size_t>(gridDim.x) * kNetBlock) {
+        const size_t r = i / ld;
+        const int c = static_cast<int>(i - r * ld);
+        if (c >= col) buf[i] = c == col ? 1.0f : 0.0f;
+        else if (src) buf[i] = src[r * col + c];
     }
 }
 
-// One env per workgroup, rows strided over its threads: logits + b_out, the
-// row-max-stabilised softmax (utils_math.py:51-63), -log(p_y + 1e-16)
+// relu in place over whole augmented buffers (the ones column stays 1, the
+// padding 0): the epilogue of a hidden layer when no hipBLASLt solution fits
+__global__ __launch_bounds__(kNetBlock) void net_relu_kernel(float *H, size_t n) {
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; i < n;
+         i += static_cast<size_t>(gridDim.x) * kNetBlock)
+        H[i] = fmaxf(H[i], 0.0f);
+}
+
+// One env per workgroup, rows strided over its threads: the logits (their
+// bias is in the augmented GEMM), the row-max-stabilised softmax (utils_math.py:51-63), -log(p_y + 1e-16)
 // (utils_math.py:25-34), np.argmax's first maximum of P, and (when dz is
 // set) dZ = P - Y in place.  Per-env sums: the cross-entropy terms in
 // float64 and the hits.  Labels: y + e * y_stride (0: the shared labels).
 __global__ __launch_bounds__(kNetBlock) void net_softmax_kernel(float *Z, int R, int K,
-                                                              const float *W, int64_t P,
-                                                              int64_t offb, const int32_t *y,
-                                                              int64_t y_stride, bool dz,
-                                                              double *loss_out, int32_t *hits_out) {
+                                                              const int32_t *y, int64_t y_stride,
+                                                              bool dz, double *loss_out,
+                                                              int32_t *hits_out) {
     __shared__ double sl[kNetBlock];
     __shared__ int sh[kNetBlock];
     const int e = blockIdx.x;
     float *z = Z + static_cast<size_t>(e) * R * K;
     const int32_t *ye = y + static_cast<size_t>(e) * y_stride;
-    const float *b = W + static_cast<size_t>(e) * P + offb;
-    float bk[kNetMaxK];
-#pragma unroll
-    for (int k = 0; k < kNetMaxK; ++k) bk[k] = k < K ? b[k] : 0.0f;
     double loss = 0.0;
     int hits = 0;
     for (int r = threadIdx.x; r < R; r += kNetBlock) {
@@ -146,7 +153,7 @@ __global__ __launch_bounds__(kNetBlock) void net_softmax_kernel(float *Z, int R,
         float m = -INFINITY;
 #pragma unroll
         for (int k = 0; k < kNetMaxK; ++k) {
-            v[k] = k < K ? zr[k] + bk[k] : -INFINITY;
+            v[k] = k < K ? zr[k] : -INFINITY;
             m = fmaxf(m, v[k]);
         }
         float s = 0.0f;
@@ -195,18 +202,6 @@ __global__ __launch_bounds__(kNetBlock) void net_softmax_kernel(float *Z, int R,
     }
 }
 
-// db[e][j] = sum over rows of dZ[e][r][j], into the env's gradient slab
-__global__ __launch_bounds__(kNetBlock) void net_colsum_kernel(const float *dZ, int R, int d,
-                                                             float *grad, int64_t P, int64_t offb) {
-    const int e = blockIdx.y;
-    const int j = blockIdx.x * kNetBlock + threadIdx.x;
-    if (j >= d) return;
-    const float *z = dZ + static_cast<size_t>(e) * R * d + j;
-    float s = 0.0f;
-    for (int r = 0; r < R; ++r) s += z[static_cast<size_t>(r) * d];
-    grad[static_cast<size_t>(e) * P + offb + j] = s;
-}
-
 // dZ = dH * relu'(Z), relu'(Z) = (H > 0) on the post-relu activation
 __global__ __launch_bounds__(kNetBlock) void net_relu_back_kernel(float *dH, const float *H, size_t n) {
     for (size_t i = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x; i < n;
@@ -233,23 +228,38 @@ __global__ __launch_bounds__(kNetBlock) void net_epilogue_kernel(NetArgs a, cons
     const size_t t0 = static_cast<size_t>(blockIdx.x) * kNetBlock + threadIdx.x;
     const size_t stride = static_cast<size_t>(gridDim.x) * kNetBlock;
     if ((P & 1) == 0) {
+        // kNetEpi parameter pairs per thread, every load before any store
+        constexpr int kNetEpi = 2;
         const float2 *g2 = reinterpret_cast<const float2 *>(grad + base);
         double2 *G2 = reinterpret_cast<double2 *>(a.G + base);
-        for (size_t q = t0; q < P / 2; q += stride) {
-            const float2 gv = g2[q];
-            const double2 Gv = G2[q];
-            const float ga = gv.x / fb, gb = gv.y / fb;
-            const double na = static_cast<double>(ga) / (fabs(Gv.x) + 1.0);
-            const double nb = static_cast<double>(gb) / (fabs(Gv.y) + 1.0);
-            const size_t p = 2 * q;
-            obs[p] = 0.0f;                                // wght_hist is identically 0
-            obs[p + 1] = 0.0f;
-            obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(na);
-            obs[P + 2 + p] = wipe ? 0.0f : static_cast<float>(nb);
-            G2[q] = wipe ? double2{0.0, 0.0} : double2{na, nb};
-            if (wipe)
-                reinterpret_cast<float2 *>(a.W + base)[q] =
-                    reinterpret_cast<const float2 *>(a.W0 + base)[q];
+        const size_t P2 = P / 2;
+        for (size_t q0 = t0; q0 < P2; q0 += kNetEpi * stride) {
+            float2 gv[kNetEpi];
+            double2 Gv[kNetEpi];
+#pragma unroll
+            for (int u = 0; u < kNetEpi; ++u) {
+                const size_t q = q0 + u * stride;
+                const size_t qc = q < P2 ? q : q0;
+                gv[u] = g2[qc];
+                Gv[u] = G2[qc];
+            }
+#pragma unroll
+            for (int u = 0; u < kNetEpi; ++u) {
+                const size_t q = q0 + u * stride;
+                if (q >= P2) break;
+                const float ga = gv[u].x / fb, gb = gv[u].y / fb;
+                const double na = static_cast<double>(ga) / (fabs(Gv[u].x) + 1.0);
+                const double nb = static_cast<double>(gb) / (fabs(Gv[u].y) + 1.0);
+                const size_t p = 2 * q;
+                obs[p] = 0.0f;                            // wght_hist is identically 0
+                obs[p + 1] = 0.0f;
+                obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(na);
+                obs[P + 2 + p] = wipe ? 0.0f : static_cast<float>(nb);
+                G2[q] = wipe ? double2{0.0, 0.0} : double2{na, nb};
+                if (wipe)
+                    reinterpret_cast<float2 *>(a.W + base)[q] =
+                        reinterpret_cast<const float2 *>(a.W0 + base)[q];
+            }
         }
         return;
     }
@@ -345,23 +355,36 @@ unsigned blocks_for(size_t n, unsigned cap) {
 
 }  // namespace
 
+// One forward GEMM of a hidden layer with its relu as the hipBLASLt
+// epilogue, descriptors and algorithm fixed at net_create
+struct LtGemm {
+    hipblasLtMatmulDesc_t op = nullptr;
+    hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, ld = nullptr;
+    hipblasLtMatmulAlgo_t algo{};
+    size_t ws = 0;
+    bool ok = false;
+};
+
 struct NetPlan {
     rocblas_handle blas = nullptr;
-    void *workspace = nullptr;
+    hipblasLtHandle_t lt = nullptr;
+    void *workspace = nullptr, *lt_workspace = nullptr;
     int nl = 0;                             // dense layers (hidden + output)
     int dims[kNetMaxHidden + 2] = {0};      // F, hidden..., K
     int64_t offW[kNetMaxHidden + 1] = {0}, offb[kNetMaxHidden + 1] = {0};
     int dmax = 0;
-    float *xb = nullptr;                    // [E][B][F] gathered minibatch rows (B < N)
+    float *xaug = nullptr;                  // [N][ld_aug(F)] the dataset rows with the ones column
+    float *xb = nullptr;                    // [E][B][ld_aug(F)] gathered minibatch rows (B < N)
     int32_t *yb = nullptr;                  // [E][B]
-    float *mb_act[kNetMaxHidden] = {nullptr};   // [E][B][d_l] hidden activations (post-relu)
+    float *mb_act[kNetMaxHidden] = {nullptr};   // [E][B][ld_aug(d_l)] hidden activations (post-relu)
     float *mb_out = nullptr;                // [E][B][K] logits, then dZ
-    float *dbuf[2] = {nullptr, nullptr};    // [E][B][dmax] dH / dZ ping-pong
+    float *dbuf[2] = {nullptr, nullptr};    // [E][B][ld_aug(dmax)] dH / dZ ping-pong
     float *grad = nullptr;                  // [E][P] summed gradient (float32)
-    float *inf[2] = {nullptr, nullptr};     // [E][N][dmax] info activations (B < N)
+    float *inf[kNetMaxHidden] = {nullptr};  // [E][N][ld_aug(d_l)] info activations (B < N)
     float *inf_out = nullptr;               // [E][N][K]
     double *mb_loss = nullptr, *inf_loss = nullptr;
     int32_t *mb_hits = nullptr, *inf_hits = nullptr;
+    LtGemm fw_mb[kNetMaxHidden], fw_inf[kNetMaxHidden];   // hidden-layer forwards (relu epilogue)
 };
 
 int64_t net_params(int F, int K, int n_hidden, const int *hidden) {
@@ -376,6 +399,8 @@ int64_t net_params(int F, int K, int n_hidden, const int *hidden) {
 }
 
 namespace {
+
+constexpr size_t kLtWorkspace = 32u << 20;
 
 // Row-major C[M][N] (row stride ldc) = op(A) op(B), op(A) M x K, op(B) K x N,
 // batched over envs with element strides (0: shared operand).  rocBLAS is
@@ -393,6 +418,78 @@ int gemm_rm(rocblas_handle h, bool tA, bool tB, int M, int N, int K, const float
         return fail(CE_EHIP, std::string("rocblas_sgemm_strided_batched failed: ") +
                                  rocblas_status_to_string(st));
     return CE_OK;
+}
+
+void lt_free(LtGemm &g) {
+    if (g.op) hipblasLtMatmulDescDestroy(g.op);
+    for (hipblasLtMatrixLayout_t l : {g.la, g.lb, g.ld})
+        if (l) hipblasLtMatrixLayoutDestroy(l);
+    g = LtGemm{};
+}
+
+hipblasLtMatrixLayout_t lt_layout(uint64_t rows, uint64_t cols, int64_t ld, int batch, int64_t stride) {
+    hipblasLtMatrixLayout_t l = nullptr;
+    if (hipblasLtMatrixLayoutCreate(&l, HIP_R_32F, rows, cols, ld) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+    const int32_t b = batch;
+    if (hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &b, sizeof(b)) !=
+            HIPBLAS_STATUS_SUCCESS ||
+        hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &stride,
+                                          sizeof(stride)) != HIPBLAS_STATUS_SUCCESS) {
+        hipblasLtMatrixLayoutDestroy(l);
+        return nullptr;
+    }
+    return l;
+}
+
+// Row-major relu(A[M][K] B[K][N]) batched: the column-major D^T (N x M) =
+// B^T (N x K) A^T (K x M), so hipBLASLt's "A" is the weight slab and its "B"
+// the activations.  g.ok stays false when the library offers no solution.
+void lt_setup(hipblasLtHandle_t h, LtGemm &g, int M, int N, int K, int lda, int64_t sA, int ldb,
+              int64_t sB, int ldc, int64_t sC, int batch) {
+    lt_free(g);
+    if (hipblasLtMatmulDescCreate(&g.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return;
+    const hipblasOperation_t nt = HIPBLAS_OP_N;
+    const hipblasLtEpilogue_t ep = HIPBLASLT_EPILOGUE_RELU;
+    if (hipblasLtMatmulDescSetAttribute(g.op, HIPBLASLT_MATMUL_DESC_TRANSA, &nt, sizeof(nt)) !=
+            HIPBLAS_STATUS_SUCCESS ||
+        hipblasLtMatmulDescSetAttribute(g.op, HIPBLASLT_MATMUL_DESC_TRANSB, &nt, sizeof(nt)) !=
+            HIPBLAS_STATUS_SUCCESS ||
+        hipblasLtMatmulDescSetAttribute(g.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep)) !=
+            HIPBLAS_STATUS_SUCCESS)
+        return;
+    g.la = lt_layout(N, K, ldb, batch, sB);
+    g.lb = lt_layout(K, M, lda, batch, sA);
+    g.ld = lt_layout(N, M, ldc, batch, sC);
+    if (!g.la || !g.lb || !g.ld) return;
+    hipblasLtMatmulPreference_t pref = nullptr;
+    if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return;
+    const uint64_t wmax = kLtWorkspace;
+    hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wmax,
+                                          sizeof(wmax));
+    hipblasLtMatmulHeuristicResult_t res[1];
+    int n = 0;
+    const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, g.op, g.la, g.lb, g.ld, g.ld, pref,
+                                                               1, res, &n);
+    hipblasLtMatmulPreferenceDestroy(pref);
+    if (st != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].state != HIPBLAS_STATUS_SUCCESS) return;
+    g.algo = res[0].algo;
+    g.ws = res[0].workspaceSize;
+    g.ok = g.ws <= kLtWorkspace;
+}
+
+int lt_run(hipblasLtHandle_t h, const LtGemm &g, const float *A, const float *B, float *C,
+           void *ws, hipStream_t s) {
+    const float one = 1.0f, zero = 0.0f;
+    const hipblasStatus_t st = hipblasLtMatmul(h, g.op, &one, B, g.la, A, g.lb, &zero, C, g.ld, C,
+                                               g.ld, &g.algo, ws, kLtWorkspace, s);
+    if (st != HIPBLAS_STATUS_SUCCESS) return fail(CE_EHIP, "network: hipblasLtMatmul failed");
+    return CE_OK;
+}
+
+void fill_aug(float *buf, size_t rows, int d, const float *src = nullptr) {
+    const size_t n = rows * ld_aug(d);
+    hipLaunchKernelGGL(net_aug_kernel, dim3(blocks_for(n, 8192)), dim3(kNetBlock), 0, nullptr, buf, rows,
+                       ld_aug(d), d, src);
 }
 
 }  // namespace
@@ -428,23 +525,32 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
     const size_t E = a.E, B = a.B, N = a.N;
     int rc;
     if (hipSetDevice(device) != hipSuccess) return bail(fail(CE_EHIP, "network: hipSetDevice"));
+    if ((rc = dev_alloc(&p->xaug, N * ld_aug(a.F))) != CE_OK) return bail(rc);
+    fill_aug(p->xaug, N, a.F, a.X);
     if (B < N) {
-        if ((rc = dev_alloc(&p->xb, E * B * a.F)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->xb, E * B * ld_aug(a.F))) != CE_OK) return bail(rc);
+        fill_aug(p->xb, E * B, a.F);
         if ((rc = dev_alloc(&p->yb, E * B)) != CE_OK) return bail(rc);
-        if ((rc = dev_alloc(&p->inf[0], E * N * p->dmax)) != CE_OK) return bail(rc);
-        if ((rc = dev_alloc(&p->inf[1], E * N * p->dmax)) != CE_OK) return bail(rc);
+        for (int l = 0; l < a.n_hidden; ++l) {
+            if ((rc = dev_alloc(&p->inf[l], E * N * ld_aug(p->dims[l + 1]))) != CE_OK) return bail(rc);
+            fill_aug(p->inf[l], E * N, p->dims[l + 1]);
+        }
         if ((rc = dev_alloc(&p->inf_out, E * N * a.K)) != CE_OK) return bail(rc);
         if ((rc = dev_alloc(&p->inf_loss, E)) != CE_OK) return bail(rc);
         if ((rc = dev_alloc(&p->inf_hits, E)) != CE_OK) return bail(rc);
     }
-    for (int l = 0; l < a.n_hidden; ++l)
-        if ((rc = dev_alloc(&p->mb_act[l], E * B * p->dims[l + 1])) != CE_OK) return bail(rc);
+    for (int l = 0; l < a.n_hidden; ++l) {
+        if ((rc = dev_alloc(&p->mb_act[l], E * B * ld_aug(p->dims[l + 1]))) != CE_OK) return bail(rc);
+        fill_aug(p->mb_act[l], E * B, p->dims[l + 1]);
+    }
     if ((rc = dev_alloc(&p->mb_out, E * B * a.K)) != CE_OK) return bail(rc);
-    if ((rc = dev_alloc(&p->dbuf[0], E * B * p->dmax)) != CE_OK) return bail(rc);
-    if ((rc = dev_alloc(&p->dbuf[1], E * B * p->dmax)) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->dbuf[0], E * B * ld_aug(p->dmax))) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->dbuf[1], E * B * ld_aug(p->dmax))) != CE_OK) return bail(rc);
     if ((rc = dev_alloc(&p->grad, E * static_cast<size_t>(a.P))) != CE_OK) return bail(rc);
     if ((rc = dev_alloc(&p->mb_loss, E)) != CE_OK) return bail(rc);
     if ((rc = dev_alloc(&p->mb_hits, E)) != CE_OK) return bail(rc);
+    CE_HIP(hipGetLastError());
+    CE_HIP(hipDeviceSynchronize());
     if (rocblas_create_handle(&p->blas) != rocblas_status_success)
         return bail(fail(CE_EHIP, "network: rocblas_create_handle failed"));
     // a fixed workspace, so no call allocates (hipGraph capture, ce_step_many)
@@ -453,22 +559,75 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
         return bail(fail(CE_ENOMEM, "network: workspace allocation failed"));
     if (rocblas_set_workspace(p->blas, p->workspace, kWorkspace) != rocblas_status_success)
         return bail(fail(CE_EHIP, "network: rocblas_set_workspace failed"));
+    // hidden-layer forwards with the relu epilogue (CE_NET_LT=0: rocBLAS and
+    // a relu pass instead, the A/B arm; also what a shape without a hipBLASLt
+    // solution runs)
+    const char *lt_env = std::getenv("CE_NET_LT");
+    if (!(lt_env && lt_env[0] == '0')) {
+        if (hipblasLtCreate(&p->lt) != HIPBLAS_STATUS_SUCCESS)
+            return bail(fail(CE_EHIP, "network: hipblasLtCreate failed"));
+        if (hipMalloc(&p->lt_workspace, kLtWorkspace) != hipSuccess)
+            return bail(fail(CE_ENOMEM, "network: hipBLASLt workspace allocation failed"));
+        for (int l = 0; l < a.n_hidden; ++l) {
+            const int din = p->dims[l], dout = p->dims[l + 1];
+            const int ldi = ld_aug(din), ldo = ld_aug(dout);
+            const int64_t sin = l == 0 ? (B < N ? static_cast<int64_t>(B) * ldi : 0)
+                                       : static_cast<int64_t>(B) * ldi;
+            lt_setup(p->lt, p->fw_mb[l], static_cast<int>(B), dout, din + 1, ldi, sin, dout, a.P, ldo,
+                     static_cast<int64_t>(B) * ldo, static_cast<int>(E));
+            if (B < N)
+                lt_setup(p->lt, p->fw_inf[l], static_cast<int>(N), dout, din + 1, ldi,
+                         l == 0 ? 0 : static_cast<int64_t>(N) * ldi, dout, a.P, ldo,
+                         static_cast<int64_t>(N) * ldo, static_cast<int>(E));
+        }
+    }
     *out = p;
     return CE_OK;
+}
+
+bool net_forward_lt(const NetPlan *p) {
+    for (int l = 0; l + 1 < p->nl; ++l)
+        if (!p->fw_mb[l].ok || (p->xb && !p->fw_inf[l].ok)) return false;
+    return true;
 }
 
 void net_destroy(NetPlan *p) {
     if (!p) return;
     if (p->blas) rocblas_destroy_handle(p->blas);
-    void *bufs[] = {p->workspace, p->xb, p->yb, p->mb_out, p->dbuf[0], p->dbuf[1], p->grad,
-                    p->inf[0], p->inf[1], p->inf_out, p->mb_loss, p->inf_loss, p->mb_hits,
+    for (int l = 0; l < kNetMaxHidden; ++l) {
+        lt_free(p->fw_mb[l]);
+        lt_free(p->fw_inf[l]);
+    }
+    if (p->lt) hipblasLtDestroy(p->lt);
+    void *bufs[] = {p->workspace, p->lt_workspace, p->xaug, p->xb, p->yb, p->mb_out, p->dbuf[0],
+                    p->dbuf[1], p->grad, p->inf_out, p->mb_loss, p->inf_loss, p->mb_hits,
                     p->inf_hits};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (float *b : p->mb_act)
         if (b) (void)hipFree(b);
+    for (float *b : p->inf)
+        if (b) (void)hipFree(b);
     delete p;
 }
+
+namespace {
+
+// one hidden layer's forward: relu(H_aug W_aug) into the augmented output
+int hidden_forward(NetPlan *p, const LtGemm &g, int rows, int din, int dout, const float *h, int64_t sh,
+                   const float *W, int64_t P, float *o, int E, hipStream_t s) {
+    const int ldi = ld_aug(din), ldo = ld_aug(dout);
+    if (g.ok) return lt_run(p->lt, g, h, W, o, p->lt_workspace, s);
+    int rc;
+    if ((rc = gemm_rm(p->blas, false, false, rows, dout, din + 1, h, ldi, sh, W, dout, P, o, ldo,
+                      static_cast<int64_t>(rows) * ldo, E)) != CE_OK)
+        return rc;
+    const size_t n = static_cast<size_t>(E) * rows * ldo;
+    hipLaunchKernelGGL(net_relu_kernel, dim3(blocks_for(n, 8192)), dim3(kNetBlock), 0, s, o, n);
+    return CE_OK;
+}
+
+}  // namespace
 
 int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
     const int E = a.E, B = a.B, N = a.N, K = a.K, nl = p->nl;
@@ -479,9 +638,11 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
     const size_t EP = static_cast<size_t>(E) * P;
     hipLaunchKernelGGL(net_update_kernel, dim3(blocks_for(EP, 8192)), dim3(kNetBlock), 0, s, a.W,
                        a.act, EP, a.step, E);
-    // the minibatch: gathered rows (B < N) or the shared dataset (B == N)
-    const float *x = full ? a.X : p->xb;
-    const int64_t sx = full ? 0 : static_cast<int64_t>(B) * a.F;
+    // the minibatch: gathered rows (B < N) or the shared dataset (B == N),
+    // both with the ones column
+    const int ldx = ld_aug(a.F);
+    const float *x = full ? p->xaug : p->xb;
+    const int64_t sx = full ? 0 : static_cast<int64_t>(B) * ldx;
     const int32_t *y = full ? a.label : p->yb;
     const int64_t sy = full ? 0 : B;
     if (!full)
@@ -493,60 +654,63 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
     int64_t sh = sx;
     for (int l = 0; l < nl; ++l) {
         const int din = p->dims[l], dout = p->dims[l + 1];
-        float *o = l + 1 < nl ? p->mb_act[l] : p->mb_out;
-        if ((rc = gemm_rm(p->blas, false, false, B, dout, din, h, din, sh, a.W + p->offW[l], dout, P,
-                          o, dout, static_cast<int64_t>(B) * dout, E)) != CE_OK)
+        if (l + 1 < nl) {
+            if ((rc = hidden_forward(p, p->fw_mb[l], B, din, dout, h, sh, a.W + p->offW[l], P,
+                                     p->mb_act[l], E, s)) != CE_OK)
+                return rc;
+            h = p->mb_act[l];
+            sh = static_cast<int64_t>(B) * ld_aug(dout);
+        } else if ((rc = gemm_rm(p->blas, false, false, B, dout, din + 1, h, ld_aug(din), sh,
+                                 a.W + p->offW[l], dout, P, p->mb_out, dout,
+                                 static_cast<int64_t>(B) * dout, E)) != CE_OK) {
             return rc;
-        if (l + 1 < nl)
-            hipLaunchKernelGGL(net_bias_act_kernel,
-                               dim3(blocks_for(static_cast<size_t>(B) * dout, 64), E),
-                               dim3(kNetBlock), 0, s, o, B, dout, a.W, P, p->offb[l]);
-        h = o;
-        sh = static_cast<int64_t>(B) * dout;
+        }
     }
-    hipLaunchKernelGGL(net_softmax_kernel, dim3(E), dim3(kNetBlock), 0, s, p->mb_out, B, K, a.W, P,
-                       p->offb[nl - 1], y, sy, true, p->mb_loss, p->mb_hits);
-    // backward: dW_l = H_{l-1}^T dZ_l, db_l, dH_{l-1} = dZ_l W_l^T, relu'
+    hipLaunchKernelGGL(net_softmax_kernel, dim3(E), dim3(kNetBlock), 0, s, p->mb_out, B, K, y, sy, true,
+                       p->mb_loss, p->mb_hits);
+    // backward: [dW_l; db_l] = H_{l-1,aug}^T dZ_l, dH_{l-1} = dZ_l W_l^T, relu'
     const float *dz = p->mb_out;
+    int lddz = K;
     for (int l = nl - 1; l >= 0; --l) {
         const int din = p->dims[l], dout = p->dims[l + 1];
         const float *hin = l == 0 ? x : p->mb_act[l - 1];
-        const int64_t shin = l == 0 ? sx : static_cast<int64_t>(B) * din;
-        const int64_t sdz = static_cast<int64_t>(B) * dout;
-        if ((rc = gemm_rm(p->blas, true, false, din, dout, B, hin, din, shin, dz, dout, sdz,
+        const int ldi = ld_aug(din);
+        const int64_t shin = l == 0 ? sx : static_cast<int64_t>(B) * ldi;
+        const int64_t sdz = static_cast<int64_t>(B) * lddz;
+        if ((rc = gemm_rm(p->blas, true, false, din + 1, dout, B, hin, ldi, shin, dz, lddz, sdz,
                           p->grad + p->offW[l], dout, P, E)) != CE_OK)
             return rc;
-        hipLaunchKernelGGL(net_colsum_kernel, dim3((dout + kNetBlock - 1) / kNetBlock, E),
-                           dim3(kNetBlock), 0, s, dz, B, dout, p->grad, P, p->offb[l]);
         if (l == 0) break;
         float *dh = p->dbuf[l & 1];
-        if ((rc = gemm_rm(p->blas, false, true, B, din, dout, dz, dout, sdz, a.W + p->offW[l], dout,
-                          P, dh, din, static_cast<int64_t>(B) * din, E)) != CE_OK)
+        if ((rc = gemm_rm(p->blas, false, true, B, din, dout, dz, lddz, sdz, a.W + p->offW[l], dout,
+                          P, dh, ldi, static_cast<int64_t>(B) * ldi, E)) != CE_OK)
             return rc;
-        const size_t n = static_cast<size_t>(E) * B * din;
+        const size_t n = static_cast<size_t>(E) * B * ldi;
         hipLaunchKernelGGL(net_relu_back_kernel, dim3(blocks_for(n, 8192)), dim3(kNetBlock), 0, s,
                            dh, p->mb_act[l - 1], n);
         dz = dh;
+        lddz = ldi;
     }
     // info['objective'] / ['accuracy'] on every row (B < N)
     if (!full) {
-        const float *hi = a.X;
+        const float *hi = p->xaug;
         int64_t shi = 0;
         for (int l = 0; l < nl; ++l) {
             const int din = p->dims[l], dout = p->dims[l + 1];
-            float *o = l + 1 < nl ? p->inf[l & 1] : p->inf_out;
-            if ((rc = gemm_rm(p->blas, false, false, N, dout, din, hi, din, shi, a.W + p->offW[l],
-                              dout, P, o, dout, static_cast<int64_t>(N) * dout, E)) != CE_OK)
+            if (l + 1 < nl) {
+                if ((rc = hidden_forward(p, p->fw_inf[l], N, din, dout, hi, shi, a.W + p->offW[l], P,
+                                         p->inf[l], E, s)) != CE_OK)
+                    return rc;
+                hi = p->inf[l];
+                shi = static_cast<int64_t>(N) * ld_aug(dout);
+            } else if ((rc = gemm_rm(p->blas, false, false, N, dout, din + 1, hi, ld_aug(din), shi,
+                                     a.W + p->offW[l], dout, P, p->inf_out, dout,
+                                     static_cast<int64_t>(N) * dout, E)) != CE_OK) {
                 return rc;
-            if (l + 1 < nl)
-                hipLaunchKernelGGL(net_bias_act_kernel,
-                                   dim3(blocks_for(static_cast<size_t>(N) * dout, 256), E),
-                                   dim3(kNetBlock), 0, s, o, N, dout, a.W, P, p->offb[l]);
-            hi = o;
-            shi = static_cast<int64_t>(N) * dout;
+            }
         }
-        hipLaunchKernelGGL(net_softmax_kernel, dim3(E), dim3(kNetBlock), 0, s, p->inf_out, N, K, a.W,
-                           P, p->offb[nl - 1], a.label, int64_t(0), false, p->inf_loss, p->inf_hits);
+        hipLaunchKernelGGL(net_softmax_kernel, dim3(E), dim3(kNetBlock), 0, s, p->inf_out, N, K, a.label,
+                           int64_t(0), false, p->inf_loss, p->inf_hits);
     }
     hipLaunchKernelGGL(net_epilogue_kernel, dim3(blocks_for(static_cast<size_t>(P + 1) / 2, 1024), E),
                        dim3(kNetBlock), 0, s, a, p->grad);
