@@ -32,8 +32,15 @@ void launch_multi_step(const ce::MultiArgs &a, int, hipStream_t s) {
     const size_t lds = a.H <= ce::kMultiStageH
                            ? ce::kMultiBlock / 64 * (64 / ce::Group<P>::G) * P * 3 * a.H * sizeof(float)
                            : 0;
-    hipLaunchKernelGGL(ce::multi_step_kernel<P>, dim3(multi_grid<P>(a.E)), dim3(ce::kMultiBlock),
-                       lds, s, a);
+#ifndef CE_MULTI_HC
+#define CE_MULTI_HC 1   // A/B switch: 0 runs the any-H kernel for every history length
+#endif
+    if (CE_MULTI_HC && a.H == 5)   // the reference's default history (multioptlrs.py:39)
+        hipLaunchKernelGGL((ce::multi_step_kernel<P, 5>), dim3(multi_grid<P>(a.E)),
+                           dim3(ce::kMultiBlock), lds, s, a);
+    else
+        hipLaunchKernelGGL((ce::multi_step_kernel<P, 0>), dim3(multi_grid<P>(a.E)),
+                           dim3(ce::kMultiBlock), lds, s, a);
 }
 template <int P>
 void launch_multi_reset(const ce::MultiArgs &a, int, hipStream_t s) {
@@ -169,6 +176,14 @@ int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out) {
         return fail(CE_EINVAL, "ce_multi_create: sizes must be positive");
     if (cfg->n_params < 2 || cfg->n_params % 2 || cfg->n_params > CE_MULTI_MAX_PARAMS)
         return fail(CE_EINVAL, "ce_multi_create: n_params must be even, 2..16");
+    {   // the step kernel's 32-bit element offsets: every ring plane and the
+        // observation block stay below 2^31 elements
+        const long long EP = static_cast<long long>(cfg->num_envs) * cfg->n_params;
+        const long long planes = std::max(cfg->max_history, 5);
+        if (EP * planes >= (1LL << 28) || EP * 3 * cfg->max_history >= (1LL << 28))
+            return fail(CE_EUNSUPPORTED, "ce_multi_create: num_envs * n_params * max(max_history, 5) "
+                                         "and the observation block must stay below 2^28 elements");
+    }
     const MultiEntry *kern = nullptr;
     for (const auto &k : kMulti)
         if (k.P == cfg->n_params) kern = &k;

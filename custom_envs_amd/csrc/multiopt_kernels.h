@@ -70,6 +70,19 @@ struct MultiArgs {
     int32_t *episode_len;    // [E]
 };
 
+// base[idx] with a 32-bit byte offset (idx * sizeof(T) < 2^32, which
+// ce_multi_create guarantees): the access is the uniform base in SGPRs plus
+// one VGPR offset, with no 64-bit address arithmetic per lane
+template <typename T>
+__device__ __forceinline__ T &at32(T *base, unsigned idx) {
+    return *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + idx * static_cast<unsigned>(sizeof(T)));
+}
+template <typename T>
+__device__ __forceinline__ const T &at32(const T *base, unsigned idx) {
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) +
+                                        idx * static_cast<unsigned>(sizeof(T)));
+}
+
 template <int P>
 struct Group {
     static constexpr int G = P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : 16;
@@ -186,7 +199,13 @@ __global__ __launch_bounds__(kMultiBlock) void multi_reset_kernel(MultiArgs a) {
     for (int k = 0; k < row; ++k) o[k] = -1.0f;
 }
 
-template <int P>
+// HC: the history length when known at compile time (the reference's
+// default max_history = 5, multioptlrs.py:39), 0 for any H.  The kernel is
+// latency-bound (a few waves per CU), so its time is its dynamic instruction
+// count: with HC the ring-age arithmetic is constant and every loop over the
+// history unrolls without branches, and the observation rows are staged with
+// LDS stores rather than flat stores.
+template <int P, int HC = 0>
 __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
 #pragma clang fp contract(off)
     constexpr int G = Group<P>::G;
@@ -198,7 +217,8 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     const size_t E = a.E;
     const bool env_ok = e < E;
     const bool on = env_ok && i < P;
-    const int H = a.H;
+    static_assert(HC <= kMultiStageH, "compile-time histories are staged");
+    const int H = HC ? HC : a.H;
     const int row = 3 * H;
     const size_t ec = env_ok ? e : 0;          // clamp so idle lanes read valid memory
     const int ic = i < P ? i : 0;
@@ -210,28 +230,33 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     // ---- every load of the step up front: no address depends on another
     // load (the ring slots are picked from registers once `step` is in), so
     // the wave waits for memory once instead of once per dependent round trip
-    const int step_prev = a.step[ec];
-    const float act = a.act[ec * P + r];
+    // 32-bit offsets (ce_multi_create keeps every ring plane and the
+    // observation block below 2^28 elements): every access is a uniform base
+    // in SGPRs plus one VGPR byte offset (at32), no 64-bit address arithmetic
+    const unsigned Eu = static_cast<unsigned>(E), eu = static_cast<unsigned>(ec);
+    const unsigned ep = eu * P + ic;               // this lane's [E][P] element
+    const int step_prev = at32(a.step, eu);
+    const float act = at32(a.act, eu * P + r);
     // the reset point: loaded here, not after the stores -- vmcnt counts
     // stores too, so a load issued after them would make its first use wait
     // for every one of them to complete
     const float th_init = i < P ? a.init[i] : 0.0f;
-    const float th0 = a.theta[ec * P + ic];
-    const float g0 = a.grad[ec * P + ic];
+    const float th0 = at32(a.theta, ep);
+    const float g0 = at32(a.grad, ep);
     float hl_v[kRawHist], hg_v[kRawHist], hw_v[kRawHist];
 #pragma unroll
     for (int k = 0; k < kRawHist; ++k) {
-        hl_v[k] = a.hl[k * E + ec];
-        hg_v[k] = a.hg[(k * E + ec) * P + ic];
-        hw_v[k] = a.hw[(k * E + ec) * P + ic];
+        hl_v[k] = at32(a.hl, k * Eu + eu);
+        hg_v[k] = at32(a.hg, k * Eu * P + ep);
+        hw_v[k] = at32(a.hw, k * Eu * P + ep);
     }
     double al_v[kMultiStageH], ag_v[kMultiStageH], aw_v[kMultiStageH];
 #pragma unroll
     for (int j = 0; j < kMultiStageH; ++j) {
         if (j < H) {                             // wave-uniform
-            al_v[j] = a.al[j * E + ec];
-            ag_v[j] = a.ag[(j * E + ec) * P + ic];
-            aw_v[j] = a.aw[(j * E + ec) * P + ic];
+            al_v[j] = at32(a.al, j * Eu + eu);
+            ag_v[j] = at32(a.ag, j * Eu * P + ep);
+            aw_v[j] = at32(a.aw, j * Eu * P + ep);
         }
     }
 
@@ -268,13 +293,13 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     const double adj_w = ratio(th, wp);
     const int aslot = (s - 1) % H;
     if (on) {
-        a.hg[(slot * E + e) * P + i] = g;
-        a.hw[(slot * E + e) * P + i] = th;
-        a.ag[(aslot * E + e) * P + i] = adj_g;
-        a.aw[(aslot * E + e) * P + i] = adj_w;
+        at32(a.hg, slot * Eu * P + ep) = g;
+        at32(a.hw, slot * Eu * P + ep) = th;
+        at32(a.ag, aslot * Eu * P + ep) = adj_g;
+        at32(a.aw, aslot * Eu * P + ep) = adj_w;
         if (i == 0) {
-            a.hl[slot * E + e] = loss;
-            a.al[aslot * E + e] = adj_l;
+            at32(a.hl, slot * Eu + eu) = loss;
+            at32(a.al, aslot * Eu + eu) = adj_l;
         }
     }
 
@@ -289,15 +314,18 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     const bool wipe = terminal && a.auto_reset;
 
     // ---- observation row of agent i: [w~ (H, newest first) | l~ (H) | g~ (H)]
-    const bool staged = H <= kMultiStageH;
+    const bool staged = HC || H <= kMultiStageH;
     const int span = 64 / G * P * row;       // floats of one wave's env block
     float *lds = stage + wave * span;
-    float *dst = staged ? lds + ((lane / G) * P + r) * row : a.obs + (ec * P + r) * row;
+    float *const lrow = lds + ((lane / G) * P + r) * row;
+    float *dst = HC ? lrow : staged ? lrow : a.obs + (eu * P + r) * static_cast<unsigned>(row);
     // slot j holds the entry of age k = (s - 1 - j) mod H (age 0 = this
     // step's, written above); ages >= s are the reset zeros
     double st_abs = 0.0;
+    // one runtime division by H: the ages step down from k0 = (s - 1) mod H
+    const int k0 = aslot;
     auto put = [&](int j, double wk, double gk, double lk) {
-        const int k = ((s - 1 - j) % H + H) % H;
+        const int k = k0 - j >= 0 ? k0 - j : k0 - j + H;   // j < H
         if (k == 0) {
             wk = adj_w;
             gk = adj_g;
@@ -316,7 +344,7 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     for (int j = 0; j < kMultiStageH; ++j)
         if (j < H) put(j, aw_v[j], ag_v[j], al_v[j]);
     for (int j = kMultiStageH; j < H; ++j)       // long histories: loaded here
-        put(j, a.aw[(j * E + ec) * P + ic], a.ag[(j * E + ec) * P + ic], a.al[j * E + ec]);
+        put(j, at32(a.aw, j * Eu * P + ep), at32(a.ag, j * Eu * P + ep), at32(a.al, j * Eu + eu));
     if (staged) {
         // the wave's rows are obs[e_first * P * row ...] contiguous
         __syncthreads();                        // every thread gets here (no early exit)
@@ -341,7 +369,7 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     const double st_all = group_sum<G>(mine * st_abs);
     if (on) {
         if (i == 0) {
-            float *info = a.info + e * kMultiInfo;
+            float *info = a.info + eu * kMultiInfo;
             info[0] = terminal ? loss : __builtin_nanf("");          // loss (None -> NaN)
             info[1] = loss;                                           // batch_loss
             info[2] = static_cast<float>(wsum / P);                   // weights_mean
@@ -356,10 +384,10 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
             info[11] = static_cast<float>(adj_l);                     // adjusted_loss
             info[12] = static_cast<float>(adjg);                      // adjusted_grad
             info[13] = static_cast<float>(gdiff);                     // grad_diff
-            a.episode_len[e] = s;
+            at32(a.episode_len, eu) = s;
         }
-        a.reward[e * P + r] = static_cast<float>(reward);
-        a.done[e * P + r] = terminal ? 1 : 0;
+        at32(a.reward, eu * P + r) = static_cast<float>(reward);
+        at32(a.done, eu * P + r) = terminal ? 1 : 0;
     }
 
     float g_init, l_init;
@@ -367,9 +395,9 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     if (wipe && on) {
         multi_store_reset<P>(a, e, i, th_init, g_init, l_init);
     } else if (on) {
-        a.theta[e * P + i] = th;
-        a.grad[e * P + i] = g;
-        if (i == 0) a.step[e] = s;
+        at32(a.theta, ep) = th;
+        at32(a.grad, ep) = g;
+        if (i == 0) at32(a.step, eu) = s;
     }
 }
 
