@@ -66,7 +66,8 @@ struct ce_multi_engine {
     hipStream_t own_stream = nullptr, stream = nullptr;
     int32_t agent_row[ce::kMultiMaxP] = {};   // output row of each agent (sorted names)
     float *theta = nullptr, *grad = nullptr, *hl = nullptr, *hg = nullptr, *hw = nullptr;
-    double *al = nullptr, *ag = nullptr, *aw = nullptr;
+    float *ol = nullptr, *og = nullptr, *ow = nullptr;   // adjusted history, observation form
+    double *sa = nullptr;                               // its per-entry |.| sums
     int32_t *step = nullptr;
     float *d_act = nullptr, *h_act = nullptr;
     size_t off[5] = {0};
@@ -96,16 +97,19 @@ ce::MultiArgs make_args(const ce_multi_engine *e, const float *act, const ce_mul
     a.auto_reset = e->cfg.auto_reset;
     for (int i = 0; i < ce::kMultiMaxP; ++i) {
         a.init[i] = i < e->cfg.n_params ? e->cfg.initial_points[i] : 0.0f;
+        a.init_g[i] = 0.0f;
         a.agent_row[i] = e->agent_row[i];
     }
+    ce::rosenbrock_ref(a.init, e->cfg.n_params, a.init_g, &a.init_l);
     a.theta = e->theta;
     a.grad = e->grad;
     a.hl = e->hl;
     a.hg = e->hg;
     a.hw = e->hw;
-    a.al = e->al;
-    a.ag = e->ag;
-    a.aw = e->aw;
+    a.ol = e->ol;
+    a.og = e->og;
+    a.ow = e->ow;
+    a.sa = e->sa;
     a.step = e->step;
     a.act = act;
     a.obs = o.obs;
@@ -214,9 +218,10 @@ int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out) {
     CE_TRY(hipMalloc(&e->hl, ce::kRawHist * E * sizeof(float)));
     CE_TRY(hipMalloc(&e->hg, ce::kRawHist * P * E * sizeof(float)));
     CE_TRY(hipMalloc(&e->hw, ce::kRawHist * P * E * sizeof(float)));
-    CE_TRY(hipMalloc(&e->al, H * E * sizeof(double)));
-    CE_TRY(hipMalloc(&e->ag, H * P * E * sizeof(double)));
-    CE_TRY(hipMalloc(&e->aw, H * P * E * sizeof(double)));
+    CE_TRY(hipMalloc(&e->ol, H * E * sizeof(float)));
+    CE_TRY(hipMalloc(&e->og, H * P * E * sizeof(float)));
+    CE_TRY(hipMalloc(&e->ow, H * P * E * sizeof(float)));
+    CE_TRY(hipMalloc(&e->sa, H * P * E * sizeof(double)));
     CE_TRY(hipMalloc(&e->step, E * sizeof(int32_t)));
     CE_TRY(hipMalloc(&e->d_act, E * P * sizeof(float)));
     CE_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_act), E * P * sizeof(float)));
@@ -249,7 +254,7 @@ void ce_multi_destroy(ce_multi_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     e->graphs.release();
     void *dev[] = {e->theta, e->grad, e->hl, e->hg, e->hw,
-                   e->al, e->ag, e->aw, e->step, e->d_act, e->d_out};
+                   e->ol, e->og, e->ow, e->sa, e->step, e->d_act, e->d_out};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);

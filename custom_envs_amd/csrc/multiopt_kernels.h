@@ -52,15 +52,22 @@ constexpr int kMultiStageH = 20;   // LDS-staged observation rows up to this H
 struct MultiArgs {
     int E, H, max_batches, auto_reset;
     float init[kMultiMaxP];      // initial points (agent order)
+    float init_g[kMultiMaxP];    // the problem's gradient at them (rosenbrock_ref)
+    float init_l;                // and its loss
     int agent_row[kMultiMaxP];   // output row of agent i within its env
     float *theta;            // [E][P]
     float *grad;             // [E][P] gradient at theta (newest raw entry)
     float *hl;               // [5][E]
     float *hg;               // [5][E][P]
     float *hw;               // [5][E][P]
-    double *al;              // [H][E]
-    double *ag;              // [H][E][P]
-    double *aw;              // [H][E][P]
+    // adjusted history, kept in observation form: an entry x is stored as
+    // float(clip(nan_to_num(x), +-100) - 1), the value every later
+    // observation row repeats, plus the float64 |w~| + |g~| + |l~| of the
+    // agent's entry for states_sum (multioptlrs.py:116-117)
+    float *ol;               // [H][E]    l~
+    float *og;               // [H][E][P] g~
+    float *ow;               // [H][E][P] w~
+    double *sa;              // [H][E][P] |w~| + |g~| + |l~| (raw)
     int32_t *step;           // [E]
     const float *act;        // [E][P] rows
     float *obs;              // [E][P][3H] rows
@@ -146,6 +153,24 @@ __device__ __forceinline__ void rosenbrock_lane(float th, int i, float &g, float
     loss = pair_terms_sum<G, P>(0.0f, term);
 }
 
+// rosenbrock_lane for a whole point on the host, in the same float32
+// operation order (no contraction): the reset point's gradient and loss
+inline void rosenbrock_ref(const float *th, int P, float *g, float *loss) {
+#pragma clang fp contract(off)
+    float l = 0.0f;
+    for (int q = 0; q < P / 2; ++q) {
+        const float x = th[2 * q], y = th[2 * q + 1];
+        const float d = y - x * x;
+        const float r = 1.0f - x;
+        const float term = 100.0f * (d * d) + r * r;
+        const float t = 200.0f * d;
+        g[2 * q] = -((2.0f * t) * x) - 2.0f * r;
+        g[2 * q + 1] = t;
+        l = l + term;
+    }
+    *loss = l;
+}
+
 // numpy.nan_to_num of a / |b| in float64.
 __device__ __forceinline__ double ratio(double a, double b) {
     const double q = a / fabs(b);
@@ -172,10 +197,11 @@ __device__ __forceinline__ void multi_store_reset(const MultiArgs &a, size_t e, 
         a.hw[(s * E + e) * P + i] = s == 0 ? th0 : 0.0f;
         if (i == 0) a.hl[s * E + e] = s == 0 ? l0 : 0.0f;
     }
-    for (int s = 0; s < a.H; ++s) {
-        a.ag[(s * E + e) * P + i] = 0.0;
-        a.aw[(s * E + e) * P + i] = 0.0;
-        if (i == 0) a.al[s * E + e] = 0.0;
+    for (int s = 0; s < a.H; ++s) {             // the reset zeros: obs form -1
+        a.og[(s * E + e) * P + i] = -1.0f;
+        a.ow[(s * E + e) * P + i] = -1.0f;
+        a.sa[(s * E + e) * P + i] = 0.0;
+        if (i == 0) a.ol[s * E + e] = -1.0f;
     }
     a.theta[e * P + i] = th0;
     a.grad[e * P + i] = g0;
@@ -250,13 +276,15 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
         hg_v[k] = at32(a.hg, k * Eu * P + ep);
         hw_v[k] = at32(a.hw, k * Eu * P + ep);
     }
-    double al_v[kMultiStageH], ag_v[kMultiStageH], aw_v[kMultiStageH];
+    float ol_v[kMultiStageH], og_v[kMultiStageH], ow_v[kMultiStageH];
+    double sa_v[kMultiStageH];
 #pragma unroll
     for (int j = 0; j < kMultiStageH; ++j) {
         if (j < H) {                             // wave-uniform
-            al_v[j] = at32(a.al, j * Eu + eu);
-            ag_v[j] = at32(a.ag, j * Eu * P + ep);
-            aw_v[j] = at32(a.aw, j * Eu * P + ep);
+            ol_v[j] = at32(a.ol, j * Eu + eu);
+            og_v[j] = at32(a.og, j * Eu * P + ep);
+            ow_v[j] = at32(a.ow, j * Eu * P + ep);
+            sa_v[j] = at32(a.sa, j * Eu * P + ep);
         }
     }
 
@@ -291,15 +319,22 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     const double adj_l = ratio(loss, l_prev);
     const double adj_g = ratio(g, gp);
     const double adj_w = ratio(th, wp);
+    // this step's entry in observation form, and its |.| sum (the order of
+    // the float64 adds is the one states_sum has always used)
+    const float nw = static_cast<float>(clip100(adj_w) - 1.0);
+    const float nl = static_cast<float>(clip100(adj_l) - 1.0);
+    const float ng = static_cast<float>(clip100(adj_g) - 1.0);
+    const double nsum = fabs(adj_w) + fabs(adj_g) + fabs(adj_l);
     const int aslot = (s - 1) % H;
     if (on) {
         at32(a.hg, slot * Eu * P + ep) = g;
         at32(a.hw, slot * Eu * P + ep) = th;
-        at32(a.ag, aslot * Eu * P + ep) = adj_g;
-        at32(a.aw, aslot * Eu * P + ep) = adj_w;
+        at32(a.og, aslot * Eu * P + ep) = ng;
+        at32(a.ow, aslot * Eu * P + ep) = nw;
+        at32(a.sa, aslot * Eu * P + ep) = nsum;
         if (i == 0) {
             at32(a.hl, slot * Eu + eu) = loss;
-            at32(a.al, aslot * Eu + eu) = adj_l;
+            at32(a.ol, aslot * Eu + eu) = nl;
         }
     }
 
@@ -320,31 +355,32 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     float *const lrow = lds + ((lane / G) * P + r) * row;
     float *dst = HC ? lrow : staged ? lrow : a.obs + (eu * P + r) * static_cast<unsigned>(row);
     // slot j holds the entry of age k = (s - 1 - j) mod H (age 0 = this
-    // step's, written above); ages >= s are the reset zeros
+    // step's, written above); slots not written since the reset hold the
+    // reset zeros in observation form (-1) with a zero |.| sum
     double st_abs = 0.0;
     // one runtime division by H: the ages step down from k0 = (s - 1) mod H
     const int k0 = aslot;
-    auto put = [&](int j, double wk, double gk, double lk) {
+    auto put = [&](int j, float wk, float gk, float lk, double sk) {
         const int k = k0 - j >= 0 ? k0 - j : k0 - j + H;   // j < H
         if (k == 0) {
-            wk = adj_w;
-            gk = adj_g;
-            lk = adj_l;
-        } else if (k >= s) {
-            wk = gk = lk = 0.0;
+            wk = nw;
+            gk = ng;
+            lk = nl;
+            sk = nsum;
         }
-        st_abs += fabs(wk) + fabs(gk) + fabs(lk);
+        st_abs += sk;
         if (on) {
-            dst[k] = wipe ? -1.0f : static_cast<float>(clip100(wk) - 1.0);
-            dst[H + k] = wipe ? -1.0f : static_cast<float>(clip100(lk) - 1.0);
-            dst[2 * H + k] = wipe ? -1.0f : static_cast<float>(clip100(gk) - 1.0);
+            dst[k] = wipe ? -1.0f : wk;
+            dst[H + k] = wipe ? -1.0f : lk;
+            dst[2 * H + k] = wipe ? -1.0f : gk;
         }
     };
 #pragma unroll
     for (int j = 0; j < kMultiStageH; ++j)
-        if (j < H) put(j, aw_v[j], ag_v[j], al_v[j]);
+        if (j < H) put(j, ow_v[j], og_v[j], ol_v[j], sa_v[j]);
     for (int j = kMultiStageH; j < H; ++j)       // long histories: loaded here
-        put(j, at32(a.aw, j * Eu * P + ep), at32(a.ag, j * Eu * P + ep), at32(a.al, j * Eu + eu));
+        put(j, at32(a.ow, j * Eu * P + ep), at32(a.og, j * Eu * P + ep), at32(a.ol, j * Eu + eu),
+            at32(a.sa, j * Eu * P + ep));
     if (staged) {
         // the wave's rows are obs[e_first * P * row ...] contiguous
         __syncthreads();                        // every thread gets here (no early exit)
@@ -390,8 +426,9 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
         at32(a.done, eu * P + r) = terminal ? 1 : 0;
     }
 
-    float g_init, l_init;
-    rosenbrock_lane<P>(th_init, i, g_init, l_init);     // all lanes: it shuffles
+    // the reset point's gradient and loss: the same for every env, formed
+    // once on the host (rosenbrock_ref, bit-identical to rosenbrock_lane)
+    const float g_init = i < P ? a.init_g[i] : 0.0f, l_init = a.init_l;
     if (wipe && on) {
         multi_store_reset<P>(a, e, i, th_init, g_init, l_init);
     } else if (on) {
