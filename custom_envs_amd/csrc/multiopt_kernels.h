@@ -235,7 +235,8 @@ template <int P, int HC = 0>
 __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
 #pragma clang fp contract(off)
     constexpr int G = Group<P>::G;
-    extern __shared__ float stage[];          // [waves][64 / G * P * 3H] when H <= kMultiStageH
+    extern __shared__ float4 stage4[];        // [waves][64 / G * P * 3H] floats when H <= kMultiStageH
+    float *stage = reinterpret_cast<float *>(stage4);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t gt = static_cast<size_t>(blockIdx.x) * kMultiBlock + threadIdx.x;
     const size_t e = gt / G;
@@ -267,6 +268,9 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     // stores too, so a load issued after them would make its first use wait
     // for every one of them to complete
     const float th_init = i < P ? a.init[i] : 0.0f;
+    // the reset point's gradient and loss: the same for every env, formed
+    // once on the host (rosenbrock_ref, bit-identical to rosenbrock_lane)
+    const float g_init = i < P ? a.init_g[i] : 0.0f, l_init = a.init_l;
     const float th0 = at32(a.theta, ep);
     const float g0 = at32(a.grad, ep);
     float hl_v[kRawHist], hg_v[kRawHist], hw_v[kRawHist];
@@ -326,17 +330,6 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     const float ng = static_cast<float>(clip100(adj_g) - 1.0);
     const double nsum = fabs(adj_w) + fabs(adj_g) + fabs(adj_l);
     const int aslot = (s - 1) % H;
-    if (on) {
-        at32(a.hg, slot * Eu * P + ep) = g;
-        at32(a.hw, slot * Eu * P + ep) = th;
-        at32(a.og, aslot * Eu * P + ep) = ng;
-        at32(a.ow, aslot * Eu * P + ep) = nw;
-        at32(a.sa, aslot * Eu * P + ep) = nsum;
-        if (i == 0) {
-            at32(a.hl, slot * Eu + eu) = loss;
-            at32(a.ol, aslot * Eu + eu) = nl;
-        }
-    }
 
     // ---- reward v6 + termination (multioptlrs.py:102-107)
     double reward = 1.0 - adj_l;
@@ -381,6 +374,22 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
     for (int j = kMultiStageH; j < H; ++j)       // long histories: loaded here
         put(j, at32(a.ow, j * Eu * P + ep), at32(a.og, j * Eu * P + ep), at32(a.ol, j * Eu + eu),
             at32(a.sa, j * Eu * P + ep));
+    // every loaded value is consumed (the rows staged, st_abs formed) before
+    // the first store: vmcnt counts stores too, so a load consumed after a
+    // store would wait for that store's completion
+    asm volatile("" ::"v"(st_abs) : "memory");
+    // this step's raw-history and adjusted-history entries
+    if (on) {
+        at32(a.hg, slot * Eu * P + ep) = g;
+        at32(a.hw, slot * Eu * P + ep) = th;
+        at32(a.og, aslot * Eu * P + ep) = ng;
+        at32(a.ow, aslot * Eu * P + ep) = nw;
+        at32(a.sa, aslot * Eu * P + ep) = nsum;
+        if (i == 0) {
+            at32(a.hl, slot * Eu + eu) = loss;
+            at32(a.ol, aslot * Eu + eu) = nl;
+        }
+    }
     if (staged) {
         // the wave's rows are obs[e_first * P * row ...] contiguous
         __syncthreads();                        // every thread gets here (no early exit)
@@ -390,7 +399,29 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
                                         : 0;
         const int n = static_cast<int>(envs) * P * row;
         float *out = a.obs + e_first * P * row;
-        for (int q = lane; q < n; q += 64) out[q] = lds[q];
+        // every LDS read of the block issued before its stores, 16 bytes a
+        // lane (one dependent LDS round trip per stored float measured 15 x
+        // ~100 cycles on the wave's critical path); the span is a multiple of
+        // 16 bytes, an unaligned caller pointer or ragged block takes floats
+        constexpr int kV = HC ? (64 / G * P * 3 * HC / 4 + 63) / 64 : 1;
+        if (HC && (n & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+            const float4 *src = reinterpret_cast<const float4 *>(lds);
+            float4 *dst4 = reinterpret_cast<float4 *>(out);
+            const int n4 = n >> 2;
+            float4 v[kV];
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {                // clamped, branch-free reads
+                const int q = lane + 64 * u;
+                v[u] = src[q < n4 ? q : n4 - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {                // lanes past the block rewrite its
+                const int q = lane + 64 * u;              // last 16 bytes with the same value
+                dst4[q < n4 ? q : n4 - 1] = v[u];
+            }
+        } else {
+            for (int q = lane; q < n; q += 64) out[q] = lds[q];
+        }
     }
 
     // ---- info (multioptlrs.py:112-127), float64 group reductions
@@ -426,9 +457,6 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
         at32(a.done, eu * P + r) = terminal ? 1 : 0;
     }
 
-    // the reset point's gradient and loss: the same for every env, formed
-    // once on the host (rosenbrock_ref, bit-identical to rosenbrock_lane)
-    const float g_init = i < P ? a.init_g[i] : 0.0f, l_init = a.init_l;
     if (wipe && on) {
         multi_store_reset<P>(a, e, i, th_init, g_init, l_init);
     } else if (on) {
