@@ -268,25 +268,28 @@ __device__ void nn_forward_hidden(const float *W, const float *bias, int w_in, i
 
 // logits[s][k] = b[k] + sum_j in[s][j] W[j][k] (K <= 32) on the VALU: thread
 // (sample s = t / 16, chunk t % 16) sums its w/16 units, then a 16-lane
-// butterfly.  Rows s >= nrows are computed and ignored.
-__device__ void nn_forward_logits(const float *W, const float *bias, int w_in, int K,
-                                  const float *in, int ld_in, float *z, int ld_z) {
+// butterfly.  Rows s >= nrows are computed and ignored.  Up to 4 classes
+// (the reference's iris-shaped default) take a 4-accumulator instance: the k
+// loops then run to 4, not to 32 with most of their work predicated off.
+template <int KM>
+__device__ void nn_logits_k(const float *W, const float *bias, int w_in, int K, const float *in,
+                            int ld_in, float *z, int ld_z) {
     const int t = threadIdx.x;
     const int s = t >> 4, ch = t & 15;
     const int per = w_in / 16;
-    float acc[kNnMaxK];
+    float acc[KM];
 #pragma unroll
-    for (int k = 0; k < kNnMaxK; ++k) acc[k] = 0.0f;
+    for (int k = 0; k < KM; ++k) acc[k] = 0.0f;
     for (int q = 0; q < per; ++q) {
         const int j = ch * per + q;
         const float hv = in[s * ld_in + j];
         const float *wr = W + static_cast<size_t>(j) * K;
 #pragma unroll
-        for (int k = 0; k < kNnMaxK; ++k)
+        for (int k = 0; k < KM; ++k)
             if (k < K) acc[k] = fmaf(hv, wr[k], acc[k]);
     }
 #pragma unroll
-    for (int k = 0; k < kNnMaxK; ++k) {
+    for (int k = 0; k < KM; ++k) {
         if (k < K) {
             float v = acc[k];
             v += __shfl_xor(v, 8, 16);
@@ -298,9 +301,14 @@ __device__ void nn_forward_logits(const float *W, const float *bias, int w_in, i
     }
     if (ch == 0) {
 #pragma unroll
-        for (int k = 0; k < kNnMaxK; ++k)
+        for (int k = 0; k < KM; ++k)
             if (k < K) z[s * ld_z + k] = acc[k] + bias[k];
     }
+}
+__device__ void nn_forward_logits(const float *W, const float *bias, int w_in, int K,
+                                  const float *in, int ld_in, float *z, int ld_z) {
+    if (K <= 4) nn_logits_k<4>(W, bias, w_in, K, in, ld_in, z, ld_z);
+    else nn_logits_k<kNnMaxK>(W, bias, w_in, K, in, ld_in, z, ld_z);
 }
 
 // softmax cross-entropy on the logits (tf.nn.softmax_cross_entropy_with_logits,

@@ -215,6 +215,26 @@ def test_small_networks_against_oracle(hidden):
         _check_env(ds, hidden, seed, acts[:, i * P:(i + 1) * P], rows, rec, i, 7)
 
 
+def test_many_classes_against_oracle():
+    """7 classes (past the eval kernels' compiled 4-class instance, nn_km):
+    the 32-class-bound instance of nn_grad_kernel / nn_step_kernel, with a
+    hidden width (96) that does not divide the 512-thread block."""
+    from custom_envs_amd.data import normalize, to_onehot
+    from custom_envs_amd.dataset import InMemoryDataSet
+    rs = np.random.RandomState(3)
+    labels = np.repeat(np.arange(7), 20)
+    feats = rs.normal(labels[:, None] * 0.5, 1.0, (140, 5))
+    ds = InMemoryDataSet(normalize(feats), to_onehot(labels)[0], 32)
+    seeds = [6, 11]
+    hidden = (96, 64)
+    P = 5 * 96 + 96 + 96 * 64 + 64 + 64 * 7 + 7
+    acts = _actions(12, len(seeds), P, 1.0, 2.5, 8)
+    P2, rows, rec = _run_engine(ds, hidden, seeds, acts, max_batches=9)
+    assert P2 == P
+    for i, seed in enumerate(seeds):
+        _check_env(ds, hidden, seed, acts[:, i * P:(i + 1) * P], rows, rec, i, 9)
+
+
 def test_long_history_against_oracle():
     """max_history 10: ring ages past the 8 the agent kernel keeps in
     registers are loaded at staging time."""
