@@ -143,22 +143,6 @@ constexpr int kNnStamps = 10;
 
 __device__ __forceinline__ int nn_ld(int w) { return ((w + 31) & ~31) + kNnPad; }
 
-// numpy.nan_to_num(a / |b|) in float64 for float32 a, b (utils_env.py:155-161).
-// Finite operands with b != 0 take the hardware reciprocal, one Newton step
-// and one residual correction (the IEEE quotient up to a final-rounding tie,
-// far below the float32 the result is stored as); anything else takes the
-// IEEE division of ratio().  About a third of the float64 work of the
-// division sequence.
-__device__ __forceinline__ double nn_ratio(float a, float b) {
-    const double ad = a, bd = fabs(static_cast<double>(b));
-    if (!(bd > 0.0 && bd <= 3.4028234663852886e38 && fabs(ad) <= 3.4028234663852886e38))
-        return ratio(a, b);
-    double r = __builtin_amdgcn_rcp(bd);
-    r = fma(r, fma(-bd, r, 1.0), r);
-    const double q = ad * r;
-    return fma(fma(-bd, q, ad), r, q);
-}
-
 // ---------------------------------------------------------------- LDS staging
 // Batch rows of env e: order[sel][e][cursor * B + s], s < nrows; X rows
 // zero-padded to the 32-column tile and zero for s >= nrows.
@@ -744,8 +728,8 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_rows_kernel(NnArgs a) {
         else if (k < s) lk = a.al[(((slot - k) % H + H) % H) * E + e];
         lobs[k] = static_cast<float>(clip100(lk) - 1.0);
     }
-    const double adj_w = nn_ratio(tn, to);
-    const double adj_g = nn_ratio(g, gp);
+    const double adj_w = ratio_fast(tn, to);
+    const double adj_g = ratio_fast(g, gp);
     const float ow = static_cast<float>(clip100(adj_w) - 1.0);
     const float og = static_cast<float>(clip100(adj_g) - 1.0);
     double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};

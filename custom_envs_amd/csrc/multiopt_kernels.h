@@ -179,6 +179,22 @@ __device__ __forceinline__ double ratio(double a, double b) {
     return q;
 }
 
+// numpy.nan_to_num(a / |b|) in float64 for float32 a, b (utils_env.py:155-161).
+// Finite operands with b != 0 take the hardware reciprocal, one Newton step
+// and one residual correction (the IEEE quotient up to a final-rounding tie,
+// far below the float32 the result is stored as); anything else takes the
+// IEEE division of ratio().  About a third of the float64 work of the
+// division sequence.
+__device__ __forceinline__ double ratio_fast(float a, float b) {
+    const double ad = a, bd = fabs(static_cast<double>(b));
+    if (!(bd > 0.0 && bd <= 3.4028234663852886e38 && fabs(ad) <= 3.4028234663852886e38))
+        return ratio(a, b);
+    double r = __builtin_amdgcn_rcp(bd);
+    r = fma(r, fma(-bd, r, 1.0), r);
+    const double q = ad * r;
+    return fma(fma(-bd, q, ad), r, q);
+}
+
 __device__ __forceinline__ double clip100(double v) {
     if (v != v) v = 0.0;
     return v < -100.0 ? -100.0 : (v > 100.0 ? 100.0 : v);
@@ -320,9 +336,9 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
             gsum += hg_v[k];
         }
     }
-    const double adj_l = ratio(loss, l_prev);
-    const double adj_g = ratio(g, gp);
-    const double adj_w = ratio(th, wp);
+    const double adj_l = ratio_fast(loss, static_cast<float>(l_prev));
+    const double adj_g = ratio_fast(g, gp);
+    const double adj_w = ratio_fast(th, wp);
     // this step's entry in observation form, and its |.| sum (the order of
     // the float64 adds is the one states_sum has always used)
     const float nw = static_cast<float>(clip100(adj_w) - 1.0);
