@@ -6,6 +6,7 @@ hipcc compiles the kernels for gfx950 only (no host fallback, no other
 arch); seeding.cpp is plain host C++.  The library has no torch dependency:
 Python binds it with ctypes (custom_envs_amd/_native.py).
 """
+import glob
 import os
 import shutil
 import subprocess
@@ -33,10 +34,9 @@ def sources():
 
 
 def headers():
-    return [os.path.join(CSRC, f) for f in ('optimize_kernels.h', 'optimize_pair_kernel.h',
-                                            'optimize_mfma_kernel.h', 'optimize_mfma.h', 'optimize_lr_mfma.h',
-                                            'multiopt_kernels.h', 'mlp_kernels.h', 'multinn_kernels.h', 'net_engine.h',
-                                            'common.h', 'seeding.h')] + [
+    """Every header the sources include (all of csrc/*.h, so a new one can
+    not be missed by the up-to-date check)."""
+    return sorted(glob.glob(os.path.join(CSRC, '*.h'))) + [
         os.path.join(ROOT, 'include', 'custom_envs_amd.h')]
 
 

@@ -50,6 +50,14 @@ __host__ __device__ constexpr size_t cat_lds_bytes(int ft, int mt) {
     return 2 * gen_block_bytes(ft) + cat_z_bytes(mt);
 }
 
+// v_max_f64 of two MFMA / LDS values without fmax's canonicalising
+// v_max_f64 x, x, x on each operand (neither can be a signalling NaN)
+__device__ __forceinline__ double cat_max(double x, double y) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
 // Instances per (NK, TAIL, K): the class count is compile-time so every
 // per-wave array is sized to the units, pairs and classes it holds.
 template <int NK, bool TAIL, int K>
@@ -139,13 +147,13 @@ __global__ __launch_bounds__(kCatBlock) void optimize_cat_kernel(StepArgs<double
                 double av[NKM > 0 ? NKM : 1];
 #pragma unroll
                 for (int s = 0; s < NKM; ++s) av[s] = xs[c * RS + 4 * s + h];
+                const double xl = TAIL ? xs[c * RS + FL] : 0.0;  // row c's last feature
                 gen_d4 z[2] = {gen_d4{0.0, 0.0, 0.0, 0.0}, gen_d4{0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
                 for (int s = 0; s < NKM; ++s)
                     z[s & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[j][s], av[s], z[s & 1], 0, 0, 0);
                 z[0] += z[1];
                 if constexpr (TAIL) {
-                    const double xl = xs[c * RS + FL];    // row c's last feature
 #pragma unroll
                     for (int q = 0; q < 4; ++q) z[0][q] = fma(wt[j][q], xl, z[0][q]);
                 }
@@ -159,15 +167,15 @@ __global__ __launch_bounds__(kCatBlock) void optimize_cat_kernel(StepArgs<double
         // ---- softmax: wave = env, lane = row
         {
             const double *xr = xb + lane * RS;
-            const int y = static_cast<int>(xr[RS - 1]);  // -1: rows padding N to the block
-            const bool valid = y >= 0 && env_ok;
             double zk[K];
-            double m = -INFINITY;
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                zk[k] = zb[(wave * K + k) * kCatZS + lane];
-                m = fmax(m, zk[k]);
-            }
+            for (int k = 0; k < K; ++k) zk[k] = zb[(wave * K + k) * kCatZS + lane];
+            const double yl = xr[RS - 1], xl = TAIL ? xr[FL] : 0.0;
+            const int y = static_cast<int>(yl);           // -1: rows padding N to the block
+            const bool valid = y >= 0 && env_ok;
+            double m = zk[0];
+#pragma unroll
+            for (int k = 1; k < K; ++k) m = cat_max(m, zk[k]);
             double ex[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) ex[k] = abs_clamp750(m - zk[k]);
@@ -187,7 +195,7 @@ __global__ __launch_bounds__(kCatBlock) void optimize_cat_kernel(StepArgs<double
                 py = k == y ? p : py;
                 const double d = valid ? p - (k == y ? 1.0 : 0.0) : 0.0;
                 zb[(wave * K + k) * kCatZS + lane] = d;
-                if constexpr (TAIL) gtail[k] = fma(xr[FL], d, gtail[k]);
+                if constexpr (TAIL) gtail[k] = fma(xl, d, gtail[k]);
             }
             hits += (valid && first == y) ? 1 : 0;
             prod *= valid ? py + 1e-16 : 1.0;
