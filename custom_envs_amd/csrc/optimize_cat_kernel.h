@@ -58,6 +58,27 @@ __device__ __forceinline__ double cat_max(double x, double y) {
     return r;
 }
 
+// Diagnostic builds (-DCE_DIAG): per wave, shader-clock sums of the phases
+// of every 64-row block (the stamp's own lgkmcnt(0) wait included, so these
+// are shares, not speeds): 0 top wait (own LDS-DMA + barrier 1), 1 forward,
+// 2 barrier 2, 3 softmax, 4 barrier 3, 5 gradient issue; 6 / 7 = the wave's
+// start / end s_memtime (end after its stores drain).
+#ifdef CE_DIAG
+#define CAT_MARK(k)                                                                  \
+    do {                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                           \
+        unsigned long long t_;                                                       \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");    \
+        __builtin_amdgcn_sched_barrier(0);                                           \
+        cat_acc[k] += t_ - cat_t;                                                    \
+        cat_t = t_;                                                                  \
+    } while (0)
+#else
+#define CAT_MARK(k) \
+    do {            \
+    } while (0)
+#endif
+
 // Instances per (NK, TAIL, K): the class count is compile-time so every
 // per-wave array is sized to the units, pairs and classes it holds.
 template <int NK, bool TAIL, int K>
@@ -130,10 +151,16 @@ __global__ __launch_bounds__(kCatBlock) void optimize_cat_kernel(StepArgs<double
                     (__attribute__((address_space(3))) void *)(dst + ch * kWave * 16), 16, 0, 0);
         }
     };
+#ifdef CE_DIAG
+    unsigned long long cat_acc[6] = {0, 0, 0, 0, 0, 0}, cat_t0, cat_t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(cat_t0)::"memory");
+    cat_t = cat_t0;
+#endif
     stage(0, 0);
     for (int jb = 0; jb < nblk; ++jb) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's part of block jb
         __syncthreads();                                   // all of it; block jb-1 consumed
+        CAT_MARK(0);
         if (jb + 1 < nblk) stage(jb + 1, (jb + 1) & 1);
         const double *xb = reinterpret_cast<const double *>(smem + (jb & 1) * kBlk);
 
@@ -162,7 +189,9 @@ __global__ __launch_bounds__(kCatBlock) void optimize_cat_kernel(StepArgs<double
                 for (int q = 0; q < 4; ++q) zb[(16 * mt + h + 4 * q) * kCatZS + 16 * sb + c] = z[0][q];
             }
         }
+        CAT_MARK(1);
         __syncthreads();
+        CAT_MARK(2);
 
         // ---- softmax: wave = env, lane = row
         {
@@ -205,7 +234,9 @@ __global__ __launch_bounds__(kCatBlock) void optimize_cat_kernel(StepArgs<double
                 since = 0;
             }
         }
+        CAT_MARK(3);
         __syncthreads();
+        CAT_MARK(4);
 
         // ---- gradient: pairs p = FTM-major (ft = p / MT, ct = p % MT)
 #pragma unroll
@@ -221,6 +252,7 @@ __global__ __launch_bounds__(kCatBlock) void optimize_cat_kernel(StepArgs<double
                 }
             }
         }
+        CAT_MARK(5);
     }
     __syncthreads();                                      // every wave done with Z
 
@@ -246,7 +278,23 @@ __global__ __launch_bounds__(kCatBlock) void optimize_cat_kernel(StepArgs<double
         }
     }
     __syncthreads();
+#ifdef CE_DIAG
+    const auto cat_diag = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned long long t_;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+        const int row = blockIdx.x * kCatWaves + wave;
+        if (row < a.E && lane < 8)
+            a.diag[static_cast<size_t>(row) * 8 + lane] =
+                lane < 6 ? cat_acc[lane] : lane == 6 ? cat_t0 : t_;
+    };
+    if (!env_ok) {
+        cat_diag();
+        return;
+    }
+#else
     if (!env_ok) return;
+#endif
 
     // ---- env e = me: totals, recurrences (optimize.py:78-92), outputs
     const int e = me;
@@ -287,6 +335,9 @@ __global__ __launch_bounds__(kCatBlock) void optimize_cat_kernel(StepArgs<double
         }
     }
     if (wipe) reset_env_rt(a, e, lane, P);
+#ifdef CE_DIAG
+    cat_diag();
+#endif
 }
 
 }  // namespace ce

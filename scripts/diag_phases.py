@@ -26,7 +26,7 @@ def main():
     p.add_argument('--envs', type=int, default=4096)
     p.add_argument('--precision', default='f64')
     p.add_argument('--steps', type=int, default=20)
-    p.add_argument('--workload', default='optimize', choices=['optimize', 'mlp'])
+    p.add_argument('--workload', default='optimize', choices=['optimize', 'mlp', 'mnist'])
     args = p.parse_args()
     assert os.environ.get('CE_LIB', '').startswith('diag'), 'run with CE_LIB=diag*'
     import torch
@@ -40,6 +40,10 @@ def main():
         from bench import mlp_dataset
         features, targets = mlp_dataset()
         eng = OptimizeEngine(features, targets, num_envs=E, batch_size=32, model='mlp')
+    elif args.workload == 'mnist':
+        from bench import mnist_dataset
+        features, targets = mnist_dataset()
+        eng = OptimizeEngine(features, targets, num_envs=E, precision='f64')
     else:
         seq = load_data('gaussians_256x10', batch_size=None)
         eng = OptimizeEngine(seq.features, seq.targets, num_envs=E, precision=args.precision)
@@ -63,6 +67,19 @@ def main():
         st = st[st[:, 0] != 0]                      # rows = workgroups x waves (4, 8 or 16)
         names = ['W + first tile loads', 'row tiles', 'partials meet', 'scalar epilogue',
                  'param epilogue + drain']
+    if 'optimize_cat_kernel' in eng.step_kernel:
+        # class-concatenated kernel: slots 0-5 = per-phase sums over the
+        # 64-row blocks, 6 / 7 = the wave's start / end s_memtime
+        names = ['top wait (LDS-DMA + barrier 1)', 'forward', 'barrier 2', 'softmax', 'barrier 3',
+                 'gradient issue']
+        res['kernel'] = eng.step_kernel
+        total = st[:, 7] - st[:, 6]
+        res['wave_total_median'] = float(np.median(total))
+        for k, name in enumerate(names):
+            res[name] = {'median': float(np.median(st[:, k])),
+                         'share': float(np.median(st[:, k] / total))}
+        print(json.dumps(res))
+        return
     if 'mlp' in eng.step_kernel:
         # mlp_step_kernel: train half stamps 0-3, info half 4-6 of the same env
         names = ['forward', 'softmax + small grads', 'dW1 + G/obs', 'train end -> info start',
