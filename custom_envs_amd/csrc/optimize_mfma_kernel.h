@@ -211,7 +211,11 @@ __global__ __launch_bounds__(kWave *kGenResetWaves) void optimize_reset_rt_kerne
 // Z^T = sum over k of W'^T_k X^T_k as kGenChains independent accumulator
 // chains (a dependent f64 MFMA waits out the previous one's latency; two
 // chains keep the matrix pipe issuing), added at the end.
+#ifdef CE_GEN_CHAINS
+constexpr int kGenChains = CE_GEN_CHAINS;
+#else
 constexpr int kGenChains = 2;
+#endif
 template <int NK>
 __device__ __forceinline__ gen_d4 gen_forward(const double (&wb)[NK], const double (&av)[NK]) {
     gen_d4 z[kGenChains];
