@@ -978,9 +978,10 @@ def net_flops(dims, B, N):
 
 
 def net_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
-    """The layered network path: every layer's product is a strided-batched
-    rocBLAS sgemm over the envs (MFMA), the rest hand-written kernels; the
-    roofline is the MFMA rate over the step's algorithmic FLOPs."""
+    """The layered network path on the hand-written MFMA kernels of
+    csrc/net_kernels.h; the roofline is the MFMA rate over the step's
+    algorithmic FLOPs (the reference's: minibatch forward + backward + the
+    full-data info forward)."""
     dims = (784,) + tuple(args.hidden) + (10,)
     P = eng.act_dim
     train_f, info_f = net_flops(dims, args.batch_size, 1024)
@@ -1005,10 +1006,12 @@ def net_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
         'roofline': {
             'bound': 'mfma', 'achieved': achieved, 'peak': MFMA_F32_PEAK_TFLOPS,
             'unit': 'TFLOP/s', 'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': None,
-            'kernel': 'one step = %s: strided-batched f32 GEMMs per layer, bias by a ones '
-                      'column (hidden forwards on hipBLASLt with the relu epilogue when :lt; '
-                      'dW/db, dH, output layer on rocBLAS) + net_update/gather/softmax/'
-                      'relu_back/epilogue/finish kernels' % eng.step_kernel,
+            'kernel': 'one step = %s: net_update (W - a into the weight image) + '
+                      'net_fwd (every row, whole layer chain in 16x16x4 f32 MFMA accumulators, '
+                      'weights by LDS-DMA; the minibatch rows keep their activations, so the '
+                      'minibatch forward is not re-run) + net_bwd (dH per hidden layer) + '
+                      'net_grad ([dW; db] on 32x32x2 MFMA with the float64 G/obs epilogue '
+                      'from the accumulators) + net_finish; no BLAS library' % eng.step_kernel,
             'flops_per_env_step': train_f + info_f, 'info_flops_per_env_step': info_f,
             'step_ms_median': kernel_ms, 'step_ms_mean': kernel_ms_mean,
         },

@@ -96,10 +96,8 @@ def _compile(out, tmp, defines, verbose):
     with ThreadPoolExecutor(max_workers=min(len(cmds), 8)) as pool:
         for proc in pool.map(lambda c: subprocess.run(c, check=True), cmds):
             pass
-    # rocBLAS / hipBLASLt: the layered network path's plain batched GEMMs
-    # (net_engine.hip; hipBLASLt for the forwards with the relu epilogue)
-    cmd = [hipcc, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out + '.tmp'] + objs + [
-        '-L/opt/rocm/lib', '-lrocblas', '-lhipblaslt', '-Wl,-rpath,/opt/rocm/lib']
+    # no BLAS library: every dense product is one of the engine's own MFMA kernels
+    cmd = [hipcc, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', out + '.tmp'] + objs
     subprocess.run(cmd, check=True)
     os.replace(out + '.tmp', out)
     return out

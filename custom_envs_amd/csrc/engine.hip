@@ -93,6 +93,7 @@ struct ce_engine {
     int P = 0, obs_dim = 0;
     bool mlp = false;  // CE_PROBLEM_MLP
     ce::NetPlan *net = nullptr;   // CE_PROBLEM_MLP on the layered path (net_engine.hip)
+    ce::NetGeom net_geo{};        // its weight-image geometry: W / W0 are [E][Pimg] images
     std::vector<int> dims;        // network: F, hidden..., K
     bool mlp_split = false;  // two launches per step (CE_MLP_SPLIT=1 or CE_MLP_PHASES)
     int mlp_phases = 3;  // bit 0: train kernel, bit 1: info kernel (CE_MLP_PHASES, profiling)
@@ -351,6 +352,31 @@ int download_typed(ce_engine *e, double *dst, const void *src, size_t count, siz
     return CE_OK;
 }
 
+// The network path's weight images <-> the flat float64 vectors of ce_state
+int net_download(ce_engine *e, double *dst, const void *img) {
+    const size_t E = e->cfg.num_envs, P = e->P, PI = static_cast<size_t>(e->net_geo.Pimg);
+    std::vector<float> tmp(E * PI), flat(P);
+    CE_HIP(hipMemcpyAsync(tmp.data(), img, E * PI * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    CE_HIP(hipStreamSynchronize(e->stream));
+    for (size_t i = 0; i < E; ++i) {
+        ce::net_image_to_flat(e->net_geo, &tmp[i * PI], flat.data());
+        for (size_t p = 0; p < P; ++p) dst[i * P + p] = flat[p];
+    }
+    return CE_OK;
+}
+
+int net_upload(ce_engine *e, void *img, const double *src) {
+    const size_t E = e->cfg.num_envs, P = e->P, PI = static_cast<size_t>(e->net_geo.Pimg);
+    std::vector<float> tmp(E * PI), flat(P);
+    for (size_t i = 0; i < E; ++i) {
+        for (size_t p = 0; p < P; ++p) flat[p] = static_cast<float>(src[i * P + p]);
+        ce::net_flat_to_image(e->net_geo, flat.data(), &tmp[i * PI]);
+    }
+    CE_HIP(hipMemcpyAsync(img, tmp.data(), E * PI * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    CE_HIP(hipStreamSynchronize(e->stream));
+    return CE_OK;
+}
+
 void copy_out(const ce_engine *e, const ce_outputs &src, const ce_outputs *dst) {
     const size_t E = e->cfg.num_envs;
     if (!dst) return;
@@ -462,8 +488,11 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
                            cfg->n_features % 8 == 0 && cfg->n_classes <= ce::kMlpMaxK &&
                            cfg->n_rows % 64 == 0 && cfg->batch_size < cfg->n_rows;
         net_path = !fused;
-        if (net_path && cfg->n_classes > 32)
-            return fail(CE_EUNSUPPORTED, "ce_create: the network takes at most 32 classes");
+        if (net_path) {   // the hand-written network kernels' limits (net_engine.h)
+            ce::NetGeom geo;
+            const int rc = ce::net_geometry(static_cast<int>(dims.size()) - 2, dims.data(), &geo);
+            if (rc != CE_OK) return rc;
+        }
     } else {
         // a register-path instance when the shape has one (unless CE_GENERIC=1
         // forces the runtime-shape kernel, for tests), else the MFMA kernel
@@ -564,9 +593,20 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
         CE_TRY(hipMalloc(&e->X, ce::stage_bytes_total(cfg->n_features, cfg->n_rows,
                                                       static_cast<int>(e->tsize))));
     }
-    CE_TRY(hipMalloc(&e->W, E * P * e->tsize));
+    // the network path keeps W / W0 as per-env weight images (net_kernels.h),
+    // zero-padded; G stays in the flat parameter order
+    size_t wper = P;
+    if (net_path) {
+        (void)ce::net_geometry(static_cast<int>(dims.size()) - 2, dims.data(), &e->net_geo);
+        wper = static_cast<size_t>(e->net_geo.Pimg);
+    }
+    CE_TRY(hipMalloc(&e->W, E * wper * e->tsize));
     CE_TRY(hipMalloc(&e->G, E * P * e->gsize));
-    CE_TRY(hipMalloc(&e->W0, E * P * e->tsize));
+    CE_TRY(hipMalloc(&e->W0, E * wper * e->tsize));
+    if (net_path) {
+        CE_TRY(hipMemset(e->W, 0, E * wper * e->tsize));
+        CE_TRY(hipMemset(e->W0, 0, E * wper * e->tsize));
+    }
     CE_TRY(hipMalloc(&e->L, E * sizeof(double)));
     CE_TRY(hipMalloc(&e->step, E * sizeof(int32_t)));
     CE_TRY(hipMalloc(&e->d_act, E * P * sizeof(float)));
@@ -621,10 +661,8 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
             if ((rc = ce::net_create(&e->net, a, cfg->device)) != CE_OK) return bail(rc);
             std::string name = "net<";
             for (size_t i = 0; i < dims.size(); ++i) name += (i ? "," : "") + std::to_string(dims[i]);
-            // ":lt": every hidden-layer forward runs on hipBLASLt with the
-            // relu epilogue; ":relu": rocBLAS plus a relu pass (CE_NET_LT=0,
-            // or a shape without a hipBLASLt solution)
-            e->kernel_name = name + (ce::net_forward_lt(e->net) ? ">:lt" : ">:relu");
+            // ":mfma": the hand-written MFMA kernels of net_kernels.h
+            e->kernel_name = name + ">:mfma";
         }
     }
 #undef CE_TRY
@@ -763,8 +801,17 @@ int ce_seed(ce_engine *e, const uint64_t *seeds, int32_t n) {
                                         with_perm ? &perm[i * N] : nullptr);
             });
         for (auto &th : pool) th.join();
-        CE_HIP(hipMemcpyAsync(e->W0, w0.data(), E * P * sizeof(float), hipMemcpyHostToDevice,
-                              e->stream));
+        if (e->net) {   // the weight images (net_kernels.h)
+            const size_t PI = static_cast<size_t>(e->net_geo.Pimg);
+            std::vector<float> img(E * PI);
+            for (size_t i = 0; i < E; ++i) ce::net_flat_to_image(e->net_geo, &w0[i * P], &img[i * PI]);
+            CE_HIP(hipMemcpyAsync(e->W0, img.data(), E * PI * sizeof(float), hipMemcpyHostToDevice,
+                                  e->stream));
+            CE_HIP(hipStreamSynchronize(e->stream));
+        } else {
+            CE_HIP(hipMemcpyAsync(e->W0, w0.data(), E * P * sizeof(float), hipMemcpyHostToDevice,
+                                  e->stream));
+        }
         if (with_perm)
             CE_HIP(hipMemcpyAsync(e->perm, perm.data(), E * N * sizeof(int32_t),
                                   hipMemcpyHostToDevice, e->stream));
@@ -896,10 +943,15 @@ int ce_get_state(ce_engine *e, const ce_state *st) {
     const size_t E = e->cfg.num_envs, P = e->P, N = e->cfg.n_rows;
     int rc;
     CE_HIP(hipStreamSynchronize(e->stream));
-    if (st->weights && (rc = download_typed(e, st->weights, e->W, E * P, e->tsize)) != CE_OK) return rc;
+    if (e->net) {
+        if (st->weights && (rc = net_download(e, st->weights, e->W)) != CE_OK) return rc;
+        if (st->init_weights && (rc = net_download(e, st->init_weights, e->W0)) != CE_OK) return rc;
+    } else {
+        if (st->weights && (rc = download_typed(e, st->weights, e->W, E * P, e->tsize)) != CE_OK) return rc;
+        if (st->init_weights && (rc = download_typed(e, st->init_weights, e->W0, E * P, e->tsize)) != CE_OK)
+            return rc;
+    }
     if (st->grad_hist && (rc = download_typed(e, st->grad_hist, e->G, E * P, e->gsize)) != CE_OK) return rc;
-    if (st->init_weights && (rc = download_typed(e, st->init_weights, e->W0, E * P, e->tsize)) != CE_OK)
-        return rc;
     if (st->loss_hist) CE_HIP(hipMemcpy(st->loss_hist, e->L, E * sizeof(double), hipMemcpyDeviceToHost));
     if (st->step) CE_HIP(hipMemcpy(st->step, e->step, E * sizeof(int32_t), hipMemcpyDeviceToHost));
     if (st->order) {
@@ -918,16 +970,25 @@ int ce_set_state(ce_engine *e, const ce_state *st) {
     const size_t E = e->cfg.num_envs, P = e->P, N = e->cfg.n_rows;
     int rc;
     CE_HIP(hipStreamSynchronize(e->stream));
-    if (st->weights && (rc = upload_typed(e, e->W, st->weights, E * P, e->tsize)) != CE_OK) return rc;
+    if (e->net) {
+        if (st->weights && (rc = net_upload(e, e->W, st->weights)) != CE_OK) return rc;
+        if (st->init_weights && (rc = net_upload(e, e->W0, st->init_weights)) != CE_OK) return rc;
+    } else {
+        if (st->weights && (rc = upload_typed(e, e->W, st->weights, E * P, e->tsize)) != CE_OK) return rc;
+        if (st->init_weights && (rc = upload_typed(e, e->W0, st->init_weights, E * P, e->tsize)) != CE_OK)
+            return rc;
+    }
     if (st->grad_hist && (rc = upload_typed(e, e->G, st->grad_hist, E * P, e->gsize)) != CE_OK) return rc;
-    if (st->init_weights && (rc = upload_typed(e, e->W0, st->init_weights, E * P, e->tsize)) != CE_OK)
-        return rc;
     if (st->loss_hist) CE_HIP(hipMemcpy(e->L, st->loss_hist, E * sizeof(double), hipMemcpyHostToDevice));
     if (st->step) CE_HIP(hipMemcpy(e->step, st->step, E * sizeof(int32_t), hipMemcpyHostToDevice));
     if (st->order) {
         if (!e->order) return fail(CE_ESTATE, "row order is only tracked when batch_size < n_rows");
         CE_HIP(hipMemcpy(e->order, st->order, E * N * sizeof(int32_t), hipMemcpyHostToDevice));
         CE_HIP(hipMemset(e->order_sel, 0, E * sizeof(int32_t)));
+        if (e->net) {   // the minibatch slots of the new order
+            const ce::NetArgs a = make_net_args(e, nullptr, region_view(e, e->d_out));
+            if ((rc = ce::net_sync_order(e->net, a, e->stream)) != CE_OK) return rc;
+        }
     }
     CE_HIP(hipStreamSynchronize(e->stream));
     e->was_reset = true;

@@ -3,33 +3,9 @@
 // softmax, float32, any batch size 1..N (custom_envs/problems/optimize_nn.py:
 // 22-64, create_neural_net utils_tf.py:74-86; default layers (256, 256)).
 // The fused config-3 kernel (mlp_kernels.h) keeps the one shape it is
-// written for (hidden 64, B = 32); every other network runs here.
-//
-// One VecEnv.step of E envs is a fixed sequence of launches on one stream:
-//   net_update_kernel   W' = W - a (optimize.py:74-75), step += 1, and the
-//                       minibatch rows of each env gathered through its
-//                       row order (sequence[0], B < N)
-//   forward             per layer one strided-batched f32 GEMM over the E envs,
-//                       H_l = relu([H_{l-1} | 1] [W_l; b_l]): the bias by the
-//                       ones column of the augmented input, the relu as the
-//                       hipBLASLt epilogue (rocBLAS + a relu pass where no
-//                       hipBLASLt solution fits, or CE_NET_LT=0) -- the dense
-//                       products are plain library GEMMs; the per-env
-//                       parameter slabs are the GEMM batch
-//   net_softmax_kernel  softmax, -log(p_y + 1e-16), argmax hit per row, the
-//                       per-env loss / hit sums, dZ = P - Y (utils_math.py:
-//                       25-34,51-63)
-//   backward            [dW_l; db_l] = [H_{l-1} | 1]^T dZ_l straight into the
-//                       env's gradient slab (one GEMM), dH_{l-1} = dZ_l W_l^T,
-//                       relu' (net_relu_back_kernel)
-//   info (B < N)        the full-data forward for info['objective'] /
-//                       ['accuracy'] (optimize.py:94-97); B == N reuses the
-//                       minibatch numbers, as the reference computes the same
-//                       values twice
-//   net_epilogue_kernel G' = (g / B) / (|G| + 1) in float64, the observation
-//                       [0 | L' | G'], the auto-reset's W <- W0, G <- 0
-//   net_finish_kernel   per env: L', reward, done, info, episode length, and
-//                       the auto-reset's order <- order[perm], L, step
+// written for (hidden 64, B = 32); every other network runs here, on the
+// hand-written MFMA kernels of net_kernels.h (the launch sequence is listed
+// there).  Limits: 1-4 hidden layers of width <= 256, K <= 32 classes.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -40,6 +16,62 @@
 namespace ce {
 
 constexpr int kNetMaxHidden = 4;
+constexpr int kNetL = kNetMaxHidden + 1;  // dense layers: hidden + the output layer
+constexpr int kNetMaxOp = 256;            // widest padded layer (hidden widths <= 256)
+constexpr int kNetMaxClasses = 32;
+constexpr int kNetChunk = 32;             // weight rows per LDS slot of the forward
+
+// Shape of the network and of its per-env weight IMAGE (net_kernels.h).
+struct NetGeom {
+    int nl;                          // dense layers (hidden + output)
+    int din[kNetL], dout[kNetL];     // true widths
+    int op[kNetL];                   // d_out padded to a multiple of 64
+    int nchunk[kNetL];               // 32-row image chunks of layer l
+    int chunk0[kNetL + 1];           // first global chunk of layer l; chunk0[nl] = all
+    int row0[kNetL + 1];             // first image row of layer l (update kernel)
+    int bias_rel[kNetL];             // layer l's bias in the bias area (floats)
+    int bias_total;                  // floats of the bias area (multiple of 64)
+    int64_t img_off[kNetL];          // layer l's rows, floats from the env image start
+    int64_t bias_base;               // the bias area, floats from the env image start
+    int64_t flat_w[kNetL];           // layer l's kernel in the flat vector (bias at + din*dout)
+    int64_t Pimg;                    // floats per env image (multiple of 64)
+    int64_t P;                       // flat parameters
+};
+
+// Image row of input unit u of layer l.  Layer 0: the feature index.  A
+// hidden layer's input unit u = 64c + 16g + 4i + j is register i of block
+// (c, j) in lane group g of the previous layer's 16x16 accumulators; chunk
+// 2c + (j >> 1) holds the 32 units of blocks (c, j & 2), (c, (j & 2) + 1) at
+// rho = 16 (j & 1) + 4i + g.
+__host__ __device__ inline int net_img_row(int l, int u) {
+    if (l == 0) return u;
+    const int c = u >> 6, w = u & 63, j = w & 3, i = (w >> 2) & 3, g = w >> 4;
+    return (2 * c + (j >> 1)) * kNetChunk + 16 * (j & 1) + 4 * i + g;
+}
+// inverse of net_img_row
+__host__ __device__ inline int net_row_unit(int l, int q) {
+    if (l == 0) return q;
+    const int chunk = q >> 5, rho = q & 31, c = chunk >> 1, jj = chunk & 1;
+    const int j = 2 * jj + (rho >> 4), i = (rho >> 2) & 3, g = rho & 3;
+    return 64 * c + 16 * g + 4 * i + j;
+}
+// position of output unit u's bias in its layer's permuted bias block:
+// block (c, j), lane group g, register i -- one float4 per lane and block
+__host__ __device__ inline int net_bias_slot(int u) {
+    const int c = u >> 6, w = u & 63, j = w & 3, i = (w >> 2) & 3, g = w >> 4;
+    return ((c * 4 + j) * 4 + g) * 4 + i;
+}
+__host__ __device__ inline int net_bias_unit(int s) {
+    const int i = s & 3, g = (s >> 2) & 3, j = (s >> 4) & 3, c = s >> 6;
+    return 64 * c + 16 * g + 4 * i + j;
+}
+
+// dims = F, hidden..., K (n_hidden + 2 entries).  CE_OK or CE_EUNSUPPORTED
+// with the reason in ce_last_error().
+int net_geometry(int n_hidden, const int *dims, NetGeom *g);
+// one env's flat [W1 | b1 | ...] vector <-> its image (padding zero)
+void net_flat_to_image(const NetGeom &g, const float *flat, float *img);
+void net_image_to_flat(const NetGeom &g, const float *img, float *flat);
 
 struct NetArgs {
     int E, N, F, K, B, P, max_steps, auto_reset;
@@ -47,15 +79,15 @@ struct NetArgs {
     int hidden[kNetMaxHidden];
     const float *X;                // [N][F] dataset rows
     const int32_t *label;          // [N]
-    float *W;                      // [E][P] flat [W1 | b1 | W2 | b2 | ...]
-    const float *W0;               // [E][P]
-    double *G;                     // [E][P] grad_hist[idx] (float64)
+    float *W;                      // [E][Pimg] weight images
+    const float *W0;               // [E][Pimg]
+    double *G;                     // [E][P] grad_hist[idx] (float64), flat order
     double *L;                     // [E]
     int32_t *step;                 // [E]
     const int32_t *perm;           // [E][N] reset permutation (B < N)
     int32_t *order;                // [2][E][N] row order ping-pong (B < N)
     int32_t *order_sel;            // [E]
-    const float *act;              // [E][P]
+    const float *act;              // [E][P] flat
     float *obs;                    // [E][2P + 1]
     float *reward;
     uint8_t *done;
@@ -66,16 +98,17 @@ struct NetArgs {
 
 struct NetPlan;
 
-// Work buffers, the rocBLAS / hipBLASLt handles and the forward GEMMs'
-// hipBLASLt algorithms for E envs of this shape.
+// Work buffers for E envs of this shape (the dataset in MFMA operand order,
+// the minibatch slots of every row, the minibatch activations and dZ).
 int net_create(NetPlan **out, const NetArgs &shape, int device);
 void net_destroy(NetPlan *plan);
+const NetGeom &net_geom(const NetPlan *plan);
 // Stream-ordered launches of one step / one reset (no host synchronisation:
 // capturable into a hipGraph).
 int net_step(NetPlan *plan, const NetArgs &a, hipStream_t stream);
 int net_reset(NetPlan *plan, const NetArgs &a, hipStream_t stream);
-// True when every hidden-layer forward has a hipBLASLt relu-epilogue algorithm.
-bool net_forward_lt(const NetPlan *plan);
+// after ce_set_state wrote a row order: the minibatch slots of that order
+int net_sync_order(NetPlan *plan, const NetArgs &a, hipStream_t stream);
 // Flat parameter count of the network.
 int64_t net_params(int F, int K, int n_hidden, const int *hidden);
 

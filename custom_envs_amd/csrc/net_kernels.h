@@ -1,0 +1,693 @@
+// Hand-written CDNA4 kernels of the layered network path (Optimize-v0 over
+// an OptimizeNN network: custom_envs/problems/optimize_nn.py:22-64,
+// create_neural_net utils_tf.py:74-86; the env step optimize.py:69-100).
+// No library GEMM: every dense product runs on v_mfma_f32_16x16x4_f32 /
+// v_mfma_f32_32x32x2_f32 issued from these kernels.
+//
+// One VecEnv.step is five stream-ordered launches (net_engine.hip):
+//   net_update_kernel  W' = W - a into the env's weight IMAGE (below), step += 1
+//   net_fwd_kernel     the forward of every dataset row (info['objective'] /
+//                      ['accuracy'], optimize.py:94-97) -- 64 rows x one env per
+//                      workgroup, the whole layer chain in registers; the rows
+//                      of the env's minibatch (sequence[0]) also leave their
+//                      activations and dZ = P - Y, and their loss / hits: the
+//                      minibatch forward is a subset of the full-data forward
+//                      under the same W' (optimize.py:74-76 then :94-96)
+//   net_bwd_kernel     dZ_l = (dZ_{l+1} W_{l+1}^T) * relu'(H_l), one hidden
+//                      layer per launch, top down
+//   net_grad_kernel    [dW_l; db_l] = [H_{l-1} | 1]^T dZ_l on MFMA, and in the
+//                      same registers the float64 epilogue G' = (g / B) /
+//                      (|G| + 1), obs = [0 | L' | G'] (optimize.py:78-91)
+//   net_finish_kernel  per env: L', reward, done, info, the auto-reset
+//                      (utils_venv.py:31: W <- W0, order <- order[perm])
+//
+// The weight IMAGE of an env (floats, NetGeom::Pimg per env) is the layout the
+// forward streams through LDS by LDS-DMA (global_load_lds_dwordx4), one
+// 32-row chunk per slot:
+//   layer l rows  [nchunk_l * 32][op_l]: op_l = d_out rounded up to 64 (zero
+//                 columns beyond d_out); layer 0 rows are the input features
+//                 in order (zero rows past F); a hidden layer's rows are its
+//                 input units in the order the previous layer's MFMA
+//                 accumulators hold them (net_img_row), so a chunk is 32
+//                 contiguous rows and a lane's 16-byte read gives four output
+//                 blocks
+//   bias area     every layer's bias, permuted so a lane reads its four
+//                 accumulator rows of a block as one float4 (net_bias_slot)
+// The flat [W1 | b1 | W2 | b2 | ...] vector (the reference's
+// trainable_variables order, utils_common.flatten_arrays) is what the C ABI
+// hands out; the engine converts at seed / get_state / set_state.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "net_engine.h"
+
+namespace ce {
+
+constexpr int kNetWaveRows = 16;      // dataset rows per wave (16x16x4 MFMA N)
+constexpr int kNetFwdWaves = 4;
+constexpr int kNetTile = kNetWaveRows * kNetFwdWaves;   // rows per forward workgroup
+constexpr int kNetSlotFloats = kNetChunk * kNetMaxOp;  // 32 KB
+constexpr int kNetMaxBias = 4 * kNetMaxOp + 64;
+constexpr int kNetThreads = 256;
+
+typedef float net_f4 __attribute__((ext_vector_type(4)));
+typedef float net_f16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+// W' = W - a (optimize.py:74-75: one float32 subtraction, as numpy), from the
+// caller's flat action into the image; current_step += 1
+// (baseenvironment.py:30-41).  One wave per image row, four columns per lane.
+struct NetUpdArgs {
+    NetGeom g;
+    int E, P;
+    float *img;                      // [E][Pimg]
+    const float *act;                // [E][P] flat
+    int32_t *step;
+};
+
+__global__ __launch_bounds__(kNetThreads) void net_update_kernel(NetUpdArgs a) {
+    const int e = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.step[e] += 1;
+    float *img = a.img + static_cast<size_t>(e) * a.g.Pimg;
+    const float *act = a.act + static_cast<size_t>(e) * a.P;
+    const int nl = a.g.nl;
+    const int rows_w = a.g.row0[nl];
+    const int rows = rows_w + a.g.bias_total / 256 + ((a.g.bias_total & 255) ? 1 : 0);
+    constexpr int U = 4;                                    // rows in flight per wave
+    const int stride = gridDim.x * 4;
+    for (int r0 = blockIdx.x * 4 + wave; r0 < rows; r0 += U * stride) {
+        net_f4 w[U];
+        float av[U][4];
+        float *dst[U];
+        bool any[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = r0 + u * stride;
+            any[u] = false;
+            dst[u] = nullptr;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) av[u][q] = 0.0f;
+            if (r >= rows) continue;
+            int64_t p0 = -1;           // flat index of column 4 lane (weights), per column (bias)
+            int64_t pb[4] = {-1, -1, -1, -1};
+            if (r < rows_w) {
+                int l = 0;
+                while (l + 1 < nl && r >= a.g.row0[l + 1]) ++l;
+                const int q = r - a.g.row0[l];
+                const int k = net_row_unit(l, q);
+                const int v = 4 * lane;
+                if (k < a.g.din[l] && v < a.g.dout[l]) {
+                    p0 = a.g.flat_w[l] + static_cast<int64_t>(k) * a.g.dout[l] + v;
+                    dst[u] = img + a.g.img_off[l] + static_cast<int64_t>(q) * a.g.op[l] + v;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        if (v + c < a.g.dout[l]) pb[c] = p0 + c;
+                }
+            } else {
+                const int s = (r - rows_w) * 256 + 4 * lane;   // bias-area slot
+                if (s < a.g.bias_total) {
+                    int l = 0;
+                    while (l + 1 < nl && s >= a.g.bias_rel[l + 1]) ++l;
+                    dst[u] = img + a.g.bias_base + s;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int un = net_bias_unit(s + c - a.g.bias_rel[l]);
+                        if (un < a.g.dout[l])
+                            pb[c] = a.g.flat_w[l] + static_cast<int64_t>(a.g.din[l]) * a.g.dout[l] + un;
+                    }
+                }
+            }
+            if (!dst[u]) continue;
+            any[u] = true;
+            w[u] = *reinterpret_cast<const net_f4 *>(dst[u]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) av[u][c] = pb[c] >= 0 ? act[pb[c]] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (any[u])
+                *reinterpret_cast<net_f4 *>(dst[u]) =
+                    net_f4{w[u][0] - av[u][0], w[u][1] - av[u][1], w[u][2] - av[u][2], w[u][3] - av[u][3]};
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The forward.  Workgroup = one env x 64 dataset rows, 4 waves x 16 rows.
+// Hidden activations stay in MFMA accumulators: layer l's output block
+// (c, j) holds units 64c + 16g + 4i + j (lane group g, register i) for row
+// n = lane & 15, which is exactly the B operand layout of layer l + 1's
+// K steps (net_img_row), so the chain never leaves registers.  A operand:
+// the lane's 16-byte LDS read of weight row k, columns 64c + 4m .. +3 =
+// four output blocks (c, 0..3).  Weights arrive in 32-row chunks by LDS-DMA,
+// double-buffered; the chunk sequence runs across layer boundaries.
+struct NetFwdArgs {
+    NetGeom g;
+    int E, N, B, T, F16;
+    const float *img;                // [E][Pimg]
+    const float *Xt;                 // [Nt / 16][F16][64 lanes][4]: X in B-operand order
+    const int32_t *label;            // [N]
+    const int32_t *mb_slot;          // [E][N]: minibatch slot of a row or -1 (nullptr: B == N)
+    double *part_loss;               // [E][T][2]: info, minibatch
+    int32_t *part_hits;              // [E][T][2]
+    float *act_mb[kNetL];            // hidden layer l: [E][B][op_l] post-relu minibatch rows
+    float *dz_out;                   // [E][B][op_{nl-1}] P - Y of the minibatch rows
+};
+
+__device__ __forceinline__ net_f4 net_mfma16(float a, float b, net_f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float slot[2][kNetSlotFloats];
+    __shared__ __attribute__((aligned(16))) float sbias[kNetMaxBias];
+    __shared__ double red_loss[2][kNetFwdWaves];
+    __shared__ int red_hits[2][kNetFwdWaves];
+
+    // XCD-aware: blocks b and b + 8 share an XCD (MI355X_MICROARCH), so the T
+    // row tiles of one env are consecutive on ONE XCD and its L2 serves the
+    // env's weight chunks to all of them
+    const int b = blockIdx.x, xcd = b & 7, qd = b >> 3;
+    const int e = (qd / a.T) * 8 + xcd, tile = qd - (qd / a.T) * a.T;
+    if (e >= a.E) return;                                   // whole workgroup, before any barrier
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+    const int row = tile * kNetTile + wave * kNetWaveRows + n;
+    const bool rvalid = row < a.N;
+    const float *img = a.img + static_cast<size_t>(e) * a.g.Pimg;
+    const int nl = a.g.nl;
+    const int total = a.g.chunk0[nl];
+
+    for (int i = tid; i < a.g.bias_total; i += kNetThreads) sbias[i] = img[a.g.bias_base + i];
+    int slot_n = -1;
+    int yl = 0;
+    if (rvalid) {
+        slot_n = a.mb_slot ? a.mb_slot[static_cast<size_t>(e) * a.N + row] : row;
+        yl = a.label[row];
+    }
+
+    auto issue = [&](int ci) {                              // LDS-DMA of chunk ci
+        int l = 0;
+        while (l + 1 < nl && ci >= a.g.chunk0[l + 1]) ++l;
+        const int op = a.g.op[l];
+        const float *src = img + a.g.img_off[l] + static_cast<int64_t>(ci - a.g.chunk0[l]) * kNetChunk * op;
+        float *dst = &slot[ci & 1][0];
+        const int ninst = op >> 3;                          // 1 KB per wave instruction
+        for (int k = wave; k < ninst; k += kNetFwdWaves)
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void *)(src + k * 256 + lane * 4),
+                (__attribute__((address_space(3))) void *)(dst + k * 256), 16, 0, 0);
+    };
+    const int rb = tile * (kNetTile / 16) + wave;           // this wave's 16-row block of Xt
+    auto xload = [&](int lc, net_f4 *xv) {                  // layer-0 B operands of chunk lc
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int tg = 2 * lc + t;
+            xv[t] = tg < a.F16 ? *reinterpret_cast<const net_f4 *>(
+                                     a.Xt + ((static_cast<size_t>(rb) * a.F16 + tg) * 64 + lane) * 4)
+                               : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+    };
+
+    net_f4 hin[16], hout[16];
+    auto bias_init = [&](int l) {
+        const int ncg = a.g.op[l] >> 6;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                hout[c * 4 + j] = c < ncg ? *reinterpret_cast<const net_f4 *>(
+                                                &sbias[a.g.bias_rel[l] + ((c * 4 + j) * 4 + g) * 4])
+                                          : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
+    };
+
+    net_f4 xc[2], xn[2];
+    issue(0);
+    xload(0, xn);
+    __syncthreads();                                        // sbias
+    bias_init(0);
+    int ci = 0;
+
+    // ---- layer 0: K = the input features, B operand = X rows
+    {
+        const int op = a.g.op[0], ncg = op >> 6, nch = a.g.nchunk[0];
+        for (int lc = 0; lc < nch; ++lc, ++ci) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own DMA + X of chunk ci
+            __syncthreads();                                   // all of chunk ci; slot ci+1 free
+            if (ci + 1 < total) issue(ci + 1);
+            xc[0] = xn[0];
+            xc[1] = xn[1];
+            if (lc + 1 < nch) xload(lc + 1, xn);
+            const float *sl = &slot[ci & 1][0];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                if (2 * lc + t < a.F16) {                   // wave-uniform
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float bx = xc[t][q];
+                        const float *wr = sl + (16 * t + 4 * g + q) * op + 4 * n;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            if (c < ncg) {
+                                const net_f4 w4 = *reinterpret_cast<const net_f4 *>(wr + 64 * c);
+#pragma unroll
+                                for (int j = 0; j < 4; ++j)
+                                    hout[c * 4 + j] = net_mfma16(w4[j], bx, hout[c * 4 + j]);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+
+    // ---- layers 1 .. nl-1: K = the previous layer's units, from registers
+    for (int l = 0; l < nl; ++l) {
+        if (l > 0) {
+            const int op = a.g.op[l], ncg = op >> 6, nch = a.g.nchunk[l];
+#pragma unroll
+            for (int lc = 0; lc < 2 * 4; ++lc) {
+                if (lc < nch) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    if (ci + 1 < total) issue(ci + 1);
+                    const float *sl = &slot[ci & 1][0];
+                    const int cin = lc >> 1, jj = lc & 1;
+#pragma unroll
+                    for (int jl = 0; jl < 2; ++jl) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const float bx = hin[cin * 4 + 2 * jj + jl][i];
+                            const float *wr = sl + (16 * jl + 4 * i + g) * op + 4 * n;
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) {
+                                if (c < ncg) {
+                                    const net_f4 w4 = *reinterpret_cast<const net_f4 *>(wr + 64 * c);
+#pragma unroll
+                                    for (int j = 0; j < 4; ++j)
+                                        hout[c * 4 + j] = net_mfma16(w4[j], bx, hout[c * 4 + j]);
+                                }
+                            }
+                        }
+                    }
+                    ++ci;
+                }
+            }
+        }
+        if (l + 1 == nl) break;
+        // hidden layer l done: relu (optimize_nn.py: Dense(relu)), the
+        // minibatch rows' activations out, next layer's bias in the accumulators
+        const int op = a.g.op[l], ncg = op >> 6;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) hin[c * 4 + j][i] = fmaxf(hout[c * 4 + j][i], 0.0f);
+        if (slot_n >= 0) {
+            float *dst = a.act_mb[l] + (static_cast<size_t>(e) * a.B + slot_n) * op;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < ncg)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        *reinterpret_cast<net_f4 *>(dst + 64 * c + 16 * g + 4 * i) =
+                            net_f4{hin[c * 4 + 0][i], hin[c * 4 + 1][i], hin[c * 4 + 2][i], hin[c * 4 + 3][i]};
+        }
+        bias_init(l + 1);
+    }
+
+    // ---- logits -> softmax (utils_math.py:51-63), -log(p_y + 1e-16)
+    // (utils_math.py:25-34), np.argmax's first maximum of P; class 16g + 4i + j
+    // of row n sits in lane group g, so lane group 0 gathers the row
+    const int K = a.g.dout[nl - 1];
+    float z[kNetMaxClasses];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            z[4 * i + j] = hout[j][i];
+            z[16 + 4 * i + j] = __shfl_down(hout[j][i], 16);
+        }
+    double loss_r = 0.0;
+    int hit_r = 0;
+    const bool owner = g == 0 && rvalid;
+    if (owner) {
+        float m = z[0];
+#pragma unroll
+        for (int k = 1; k < kNetMaxClasses; ++k)
+            if (k < K) m = fmaxf(m, z[k]);
+        float s = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kNetMaxClasses; ++k)
+            if (k < K) {
+                z[k] = expf(z[k] - m);
+                s += z[k];
+            }
+        int arg = 0;
+        float best = -1.0f, py = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kNetMaxClasses; ++k)
+            if (k < K) {
+                z[k] = z[k] / s;                             // P
+                if (z[k] > best) {
+                    best = z[k];
+                    arg = k;
+                }
+                if (k == yl) py = z[k];
+            }
+        loss_r = static_cast<double>(-logf(py + 1e-16f));
+        hit_r = arg == yl ? 1 : 0;
+        if (slot_n >= 0) {
+            float *dz = a.dz_out + (static_cast<size_t>(e) * a.B + slot_n) * a.g.op[nl - 1];
+#pragma unroll
+            for (int k = 0; k < kNetMaxClasses; ++k)
+                if (k < K) dz[k] = z[k] - (k == yl ? 1.0f : 0.0f);
+        }
+    }
+    double lsum[2] = {loss_r, slot_n >= 0 ? loss_r : 0.0};
+    int hsum[2] = {hit_r, slot_n >= 0 ? hit_r : 0};
+#pragma unroll
+    for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            lsum[s] += __shfl_xor(lsum[s], w);
+            hsum[s] += __shfl_xor(hsum[s], w);
+        }
+    if (lane == 0)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            red_loss[s][wave] = lsum[s];
+            red_hits[s][wave] = hsum[s];
+        }
+    __syncthreads();
+    if (tid < 2) {
+        double l = 0.0;
+        int h = 0;
+#pragma unroll
+        for (int w = 0; w < kNetFwdWaves; ++w) {
+            l += red_loss[tid][w];
+            h += red_hits[tid][w];
+        }
+        const size_t o = (static_cast<size_t>(e) * a.T + tile) * 2 + tid;
+        a.part_loss[o] = l;
+        a.part_hits[o] = h;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// dH_l = dZ_{l+1} W_{l+1}^T, dZ_l = dH_l * (H_l > 0) over the minibatch rows
+// (tf.gradients of the summed cross-entropy, optimize_nn.py:48-52), for one
+// hidden layer lh; one workgroup per env.  dH^T (units x rows) on 16x16x4:
+// A = W_{l+1} rows (its image rows are the units of H_l), B = dZ_{l+1}.
+struct NetBwdArgs {
+    NetGeom g;
+    int E, B, lh;
+    const float *img;
+    const float *dz_next;            // [E][B][op_{lh+1}]
+    const float *act;                // [E][B][op_lh] post-relu H_lh
+    float *dz;                       // [E][B][op_lh]
+};
+
+__global__ __launch_bounds__(kNetThreads) void net_bwd_kernel(NetBwdArgs a) {
+    const int e = blockIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+    const int lh = a.lh, lo = lh + 1;
+    const int op = a.g.op[lh], opn = a.g.op[lo];
+    const int vend = (a.g.dout[lo] + 15) & ~15;
+    const float *W = a.img + static_cast<size_t>(e) * a.g.Pimg + a.g.img_off[lo];
+    const float *dzn = a.dz_next + static_cast<size_t>(e) * a.B * opn;
+    const float *H = a.act + static_cast<size_t>(e) * a.B * op;
+    float *dz = a.dz + static_cast<size_t>(e) * a.B * op;
+    const int nrb = (a.B + 15) >> 4, nub = op >> 4;
+    for (int t = wave; t < nrb * nub; t += kNetFwdWaves) {
+        const int rbk = t / nub, ub = t - rbk * nub;
+        const int u = 16 * ub + n, r = 16 * rbk + n;
+        const float *wr = W + static_cast<int64_t>(net_img_row(lo, u)) * opn + 4 * g;
+        const float *zr = dzn + static_cast<int64_t>(r) * opn + 4 * g;
+        const bool rok = r < a.B;
+        net_f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int v0 = 0; v0 < vend; v0 += 16) {
+            const net_f4 wv = *reinterpret_cast<const net_f4 *>(wr + v0);
+            const net_f4 zv = rok ? *reinterpret_cast<const net_f4 *>(zr + v0) : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc = net_mfma16(wv[q], zv[q], acc);
+        }
+        // acc[i] = dH[row 16 rbk + n][unit 16 ub + 4g + i]
+        if (rok) {
+            const size_t o = static_cast<size_t>(r) * op + 16 * ub + 4 * g;
+            const net_f4 h = *reinterpret_cast<const net_f4 *>(H + o);
+            *reinterpret_cast<net_f4 *>(dz + o) =
+                net_f4{h[0] > 0.0f ? acc[0] : 0.0f, h[1] > 0.0f ? acc[1] : 0.0f,
+                       h[2] > 0.0f ? acc[2] : 0.0f, h[3] > 0.0f ? acc[3] : 0.0f};
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// [dW_l; db_l] = [H_{l-1} | 1]^T dZ_l over the minibatch rows on
+// v_mfma_f32_32x32x2_f32 (the ones column gives db = sum of dZ rows), and the
+// float64 epilogue straight from the accumulators: g = grad / B (float32, as
+// numpy divides the float32 gradient), G' = g / (|G| + 1) in float64
+// (grad_hist float64, optimize.py:78-83), obs = [0 (P) | L' | G' (P)]; an env
+// whose step ends its episode (utils_venv.py:31) writes the reset
+// observation and G <- 0.  Workgroup = 32 rows of [dW; db] x 256 units of one
+// layer of one env; wave = 64 units (two 32x32 blocks).
+struct NetGradArgs {
+    NetGeom g;
+    int E, N, B, P, F, max_steps, auto_reset, tpe;
+    int task0[kNetL + 1];            // first task of layer l within an env
+    int ut[kNetL];                   // 256-unit tiles of layer l
+    const float *X;                  // [N][F]
+    const int32_t *order;            // [2][E][N] (nullptr: B == N, rows in order)
+    const int32_t *order_sel;
+    const float *act_mb[kNetL];
+    const float *dz_mb[kNetL];       // hidden layers; the output layer reads dz_out
+    const float *dz_out;
+    const int32_t *step;
+    double *G;                       // [E][P]
+    float *obs;                      // [E][2P + 1]
+};
+
+__device__ __forceinline__ net_f16 net_mfma32(float a, float b, net_f16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
+    const int e = blockIdx.x / a.tpe;
+    const int task = blockIdx.x - e * a.tpe;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, h = lane >> 5, m = lane & 31;
+    const int nl = a.g.nl;
+    int l = 0;
+    while (l + 1 < nl && task >= a.task0[l + 1]) ++l;
+    const int tl = task - a.task0[l];
+    const int kt = tl / a.ut[l], ut = tl - kt * a.ut[l];
+    const int din = a.g.din[l], dout = a.g.dout[l];
+    const int u0 = ut * 256 + 64 * wave;
+    if (u0 >= dout) return;                                 // no barriers in this kernel
+    const int k0 = kt * 32, k = k0 + m;
+    // A: [H_{l-1} | 1] rows (layer 0: the dataset rows of sequence[0])
+    const float *Hin = nullptr;
+    int hstride = 0;
+    const int32_t *rows = nullptr;
+    if (l == 0) {
+        if (a.order)
+            rows = a.order + (static_cast<size_t>(a.order_sel[e]) * a.E + e) * a.N;
+    } else {
+        hstride = a.g.op[l - 1];
+        Hin = a.act_mb[l - 1] + static_cast<size_t>(e) * a.B * hstride;
+    }
+    const int opl = a.g.op[l];
+    const float *dz = (l + 1 == nl ? a.dz_out : a.dz_mb[l]) + static_cast<size_t>(e) * a.B * opl + u0 + m;
+    net_f16 acc0 = {}, acc1 = {};
+    const int steps = (a.B + 1) >> 1;
+    for (int s = 0; s < steps; ++s) {
+        const int r = 2 * s + h;
+        float xa = 0.0f, b0 = 0.0f, b1 = 0.0f;
+        if (r < a.B) {
+            if (k < din) {
+                if (l == 0) {
+                    const int xr = rows ? rows[r] : r;
+                    xa = a.X[static_cast<size_t>(xr) * a.F + k];
+                } else {
+                    xa = Hin[static_cast<size_t>(r) * hstride + k];
+                }
+            } else if (k == din) {
+                xa = 1.0f;                                  // the bias row
+            }
+            b0 = dz[static_cast<size_t>(r) * opl];
+            b1 = dz[static_cast<size_t>(r) * opl + 32];
+        }
+        acc0 = net_mfma32(xa, b0, acc0);
+        acc1 = net_mfma32(xa, b1, acc1);
+    }
+    // epilogue: accumulator r of lane (h, m) = row k0 + 8(r>>2) + 4h + (r&3) of
+    // [dW; db], unit u0 + 32 bb + m
+    const int cur = a.step[e];
+    const bool wipe = cur >= a.max_steps && a.auto_reset;
+    const float fB = static_cast<float>(a.B);
+    const size_t P = a.P;
+    double *G = a.G + static_cast<size_t>(e) * P;
+    float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
+    const int64_t fw = a.g.flat_w[l];
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+        const int u = u0 + 32 * bb + m;
+        const net_f16 &acc = bb ? acc1 : acc0;
+        double gold[16];
+        int64_t pp[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int kk = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
+            pp[r] = (kk <= din && u < dout) ? fw + static_cast<int64_t>(kk) * dout + u : -1;
+            gold[r] = pp[r] >= 0 ? G[pp[r]] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (pp[r] < 0) continue;
+            const float gv = acc[r] / fB;
+            const double gn = static_cast<double>(gv) / (fabs(gold[r]) + 1.0);
+            obs[pp[r]] = 0.0f;                              // wght_hist is identically 0
+            obs[P + 1 + pp[r]] = wipe ? 0.0f : static_cast<float>(gn);
+            G[pp[r]] = wipe ? 0.0 : gn;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Per env: the minibatch / full-data loss and hits from the forward's tile
+// partials; L' = (loss - L)/(L + 0.1) (optimize.py:80-81), reward = -loss,
+// done = current_step >= max_steps (:102-103), info, episode length; the
+// auto-reset: W <- W0 (the image), L, step, order <- order[perm] and the
+// minibatch slots of the new order.
+struct NetFinArgs {
+    int E, N, B, P, T, max_steps, auto_reset;
+    int64_t Pimg;
+    const double *part_loss;
+    const int32_t *part_hits;
+    float *img;
+    const float *img0;
+    double *L;
+    int32_t *step;
+    const int32_t *perm;
+    int32_t *order;
+    int32_t *order_sel;
+    int32_t *mb_slot;
+    float *obs;
+    float *reward;
+    uint8_t *done;
+    float *objective;
+    float *accuracy;
+    int32_t *episode_len;
+};
+
+// order <- order[perm] (the reset's shuffle composed onto the current row
+// order) and the slot of every row in the new minibatch (-1 past B)
+__device__ inline void net_compose_order(const NetFinArgs &a, int e) {
+    const int sel = a.order_sel[e];
+    const int32_t *cur = a.order + (static_cast<size_t>(sel) * a.E + e) * a.N;
+    int32_t *nxt = a.order + (static_cast<size_t>(1 - sel) * a.E + e) * a.N;
+    const int32_t *pm = a.perm + static_cast<size_t>(e) * a.N;
+    int32_t *slots = a.mb_slot + static_cast<size_t>(e) * a.N;
+    for (int i = threadIdx.x; i < a.N; i += kNetThreads) {
+        const int32_t r = cur[pm[i]];
+        nxt[i] = r;
+        slots[r] = i < a.B ? i : -1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) a.order_sel[e] = 1 - sel;
+}
+
+__global__ __launch_bounds__(kNetThreads) void net_finish_kernel(NetFinArgs a) {
+    const int e = blockIdx.x;
+    const int cur = a.step[e];
+    const bool done = cur >= a.max_steps;
+    const bool wipe = done && a.auto_reset;
+    __syncthreads();                                        // every thread has read step[e]
+    if (threadIdx.x == 0) {
+        double lm = 0.0, li = 0.0;
+        int hm = 0, hi = 0;
+        for (int t = 0; t < a.T; ++t) {
+            const size_t o = (static_cast<size_t>(e) * a.T + t) * 2;
+            li += a.part_loss[o];
+            lm += a.part_loss[o + 1];
+            hi += a.part_hits[o];
+            hm += a.part_hits[o + 1];
+        }
+        // the loss is a float32 mean in the reference (TF / numpy float32)
+        const float loss = static_cast<float>(lm / a.B);
+        const float acc = static_cast<float>(static_cast<double>(hm) / a.B);
+        const bool full = a.B == a.N;
+        const float obj = full ? loss : static_cast<float>(li / a.N);
+        const float oacc = full ? acc : static_cast<float>(static_cast<double>(hi) / a.N);
+        const double lprev = a.L[e];
+        const double lnew = (static_cast<double>(loss) - lprev) / (lprev + 0.1);
+        const size_t P = a.P;
+        a.obs[static_cast<size_t>(e) * (2 * P + 1) + P] = wipe ? 0.0f : static_cast<float>(lnew);
+        a.reward[e] = -loss;
+        a.done[e] = done ? 1 : 0;
+        a.objective[e] = obj;
+        a.accuracy[e] = oacc;
+        a.episode_len[e] = cur;
+        a.L[e] = wipe ? 0.0 : lnew;
+        a.step[e] = wipe ? 0 : cur;
+    }
+    if (!wipe) return;
+    const size_t n4 = static_cast<size_t>(a.Pimg) >> 2;
+    net_f4 *w = reinterpret_cast<net_f4 *>(a.img + static_cast<size_t>(e) * a.Pimg);
+    const net_f4 *w0 = reinterpret_cast<const net_f4 *>(a.img0 + static_cast<size_t>(e) * a.Pimg);
+    for (size_t i = threadIdx.x; i < n4; i += kNetThreads) w[i] = w0[i];
+    if (a.order != nullptr) net_compose_order(a, e);
+}
+
+// Reset (optimize.py:58-67): W <- W0, G <- 0, obs <- 0
+struct NetResetArgs {
+    int E, P;
+    int64_t Pimg;
+    float *img;
+    const float *img0;
+    double *G;
+    float *obs;
+};
+
+__global__ __launch_bounds__(kNetThreads) void net_reset_params_kernel(NetResetArgs a) {
+    const int e = blockIdx.y;
+    const size_t P = a.P;
+    const size_t t0 = static_cast<size_t>(blockIdx.x) * kNetThreads + threadIdx.x;
+    const size_t st = static_cast<size_t>(gridDim.x) * kNetThreads;
+    float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
+    for (size_t p = t0; p < 2 * P + 1; p += st) {
+        obs[p] = 0.0f;
+        if (p < P) a.G[static_cast<size_t>(e) * P + p] = 0.0;
+    }
+    const size_t n4 = static_cast<size_t>(a.Pimg) >> 2;
+    net_f4 *w = reinterpret_cast<net_f4 *>(a.img + static_cast<size_t>(e) * a.Pimg);
+    const net_f4 *w0 = reinterpret_cast<const net_f4 *>(a.img0 + static_cast<size_t>(e) * a.Pimg);
+    for (size_t i = t0; i < n4; i += st) w[i] = w0[i];
+}
+
+// per env: L, step, and order <- order[perm] with its minibatch slots
+__global__ __launch_bounds__(kNetThreads) void net_reset_env_kernel(NetFinArgs a) {
+    const int e = blockIdx.x;
+    if (threadIdx.x == 0) {
+        a.L[e] = 0.0;
+        a.step[e] = 0;
+    }
+    if (a.order != nullptr) net_compose_order(a, e);
+}
+
+// minibatch slots of the current row order (after ce_set_state wrote one)
+__global__ __launch_bounds__(kNetThreads) void net_slots_kernel(NetFinArgs a) {
+    const int e = blockIdx.x;
+    const int32_t *cur = a.order + (static_cast<size_t>(a.order_sel[e]) * a.E + e) * a.N;
+    int32_t *slots = a.mb_slot + static_cast<size_t>(e) * a.N;
+    for (int i = threadIdx.x; i < a.N; i += kNetThreads) slots[cur[i]] = i < a.B ? i : -1;
+}
+
+}  // namespace ce

@@ -122,6 +122,58 @@ def test_config3_envs_against_live_oracle():
         eng.close()
 
 
+def test_config3_benchmark_size_sampled_envs():
+    """Config 3 at the size the bench runs it (BASELINE configs[2]: 4096
+    envs, 784 -> 64 -> 10, N = 1024, B = 32): envs 0, 1, 2047, 2048, 4094 and
+    4095 of the 4096-env grid against live oracle envs over 42 steps (one
+    auto-reset), with device-resident actions and outputs as in bench.py."""
+    import torch
+    from custom_envs_amd.data import load_data
+    seq = load_data('mnist_synthetic', batch_size=32)
+    E = 4096
+    sample = [0, 1, 2047, 2048, 4094, 4095]
+    eng = _engine(seq.features, seq.targets, E)
+    try:
+        assert eng.step_kernel == 'mlp_step_kernel'
+        eng.seed(list(range(E)))
+        P = eng.act_dim
+        out = eng.alloc_device_outputs()
+        eng.reset_device(out)
+        eng.wait()
+        refs = []
+        for s in sample:
+            env = OracleEnv(seq.features, seq.targets, batch_size=32, model='mlp')
+            env.seed(s)
+            env.reset()
+            refs.append(env)
+        gen = torch.Generator(device='cuda')
+        gen.manual_seed(1234)
+        acts = torch.empty((E, P), dtype=torch.float32, device='cuda')
+        idx = torch.tensor(sample, device='cuda')
+        for t in range(42):
+            acts.normal_(0.0, 1e-3, generator=gen)
+            torch.cuda.synchronize()
+            eng.step_device(acts, out)
+            eng.wait()
+            a = acts.index_select(0, idx).cpu().numpy()
+            obs = out['obs'].view(E, -1).index_select(0, idx).cpu().numpy()
+            got = {k: out[k].index_select(0, idx).cpu().numpy()
+                   for k in ('reward', 'done', 'objective', 'accuracy', 'episode_len')}
+            for i, env in enumerate(refs):
+                o, reward, done, info = env.step(a[i])
+                if done:
+                    o = env.reset()
+                what = 'env %d step %d' % (sample[i], t)
+                assert bool(got['done'][i]) == done, what
+                assert int(got['episode_len'][i]) == info['episode']['l'], what
+                _row_close(obs[i], o, what=what)
+                assert _rel(got['reward'][i], reward) <= RTOL, what
+                assert _rel(got['objective'][i], info['objective']) <= RTOL, what
+                assert got['accuracy'][i] == np.float32(info['accuracy']), what
+    finally:
+        eng.close()
+
+
 def test_mlp_determinism_and_episode_cycle():
     from oracle.gen_golden import mlp_dataset
     features, targets = mlp_dataset()
@@ -416,7 +468,7 @@ def test_default_network_256x256(batch_size):
     seq = load_data('mnist_synthetic', batch_size=batch_size)
     eng = _net_engine(seq.features, seq.targets, 3, (256, 256), batch_size)
     try:
-        assert eng.step_kernel == 'net<784,256,256,10>:lt'   # relu epilogue on hipBLASLt
+        assert eng.step_kernel == 'net<784,256,256,10>:mfma'   # the hand-written MFMA kernels
         _net_check(seq.features, seq.targets, eng, (256, 256), batch_size, [3, 4, 5], 42)
     finally:
         eng.close()
@@ -441,18 +493,57 @@ def test_network_shapes(hidden, batch_size, monkeypatch):
         eng.close()
 
 
-def test_network_rocblas_relu_arm(monkeypatch):
-    """CE_NET_LT=0: the hidden forwards on rocBLAS plus a relu pass (the A/B
-    arm, and what a shape without a hipBLASLt solution runs), three layers
-    with a minibatch and the default network with the full batch."""
+def test_network_full_batch_and_depth():
+    """The default network with the full batch (B = N: every row is a
+    minibatch row, the info numbers are the minibatch's), and three hidden
+    layers with a minibatch -- the shapes the rocBLAS arm used to cover."""
     from oracle.gen_golden import mlp_dataset
     features, targets = mlp_dataset()
-    monkeypatch.setenv('CE_NET_LT', '0')
     for hidden, batch_size in (((96, 32, 48), 20), ((256, 256), None)):
         eng = _net_engine(features, targets, 3, hidden, batch_size)
         try:
-            assert eng.step_kernel.endswith(':relu')
+            assert eng.step_kernel.endswith(':mfma')
             _net_check(features, targets, eng, hidden, batch_size, [7, 8, 9], 41, scale=3e-3)
+        finally:
+            eng.close()
+
+
+def test_network_state_roundtrip():
+    """ce_set_state / ce_get_state through the weight images (net_kernels.h):
+    the flat [W1 | b1 | ...] vector comes back bit for bit, odd widths
+    included, and a step from a set state matches the oracle."""
+    from oracle.gen_golden import mlp_dataset
+    features, targets = mlp_dataset()
+    for hidden in ((33, 7), (256, 256)):
+        eng = _net_engine(features, targets, 2, hidden, 24)
+        try:
+            eng.seed([1, 2])
+            eng.reset()
+            st = eng.get_state()
+            rs = np.random.RandomState(5)
+            w = rs.normal(0, 0.1, st['weights'].shape).astype(np.float32).astype(np.float64)
+            eng.set_state(weights=w, init_weights=w[::-1].copy())
+            back = eng.get_state()
+            assert np.array_equal(back['weights'], w)
+            assert np.array_equal(back['init_weights'], w[::-1])
+            # a row order written by set_state moves the minibatch (its slots)
+            perms = np.stack([rs.permutation(len(features)) for _ in range(2)]).astype(np.int32)
+            eng.set_state(order=perms)
+            assert np.array_equal(eng.get_state()['order'], perms)
+            acts = rs.normal(0, 1e-3, w.shape).astype(np.float32)
+            out = eng.step(acts)
+            from oracle.optimize import ModelMLP
+            for i in range(2):
+                model = ModelMLP(features.shape[1], targets.shape[1], hidden)
+                model.set_weights(w[i].astype(np.float32) - acts[i])
+                rows = perms[i][:24]
+                loss, grad, _ = model.compute_backprop(features[rows].astype(np.float32),
+                                                       targets[rows].astype(np.float32))
+                assert _rel(out['reward'][i], -loss) <= RTOL, (hidden, i)
+                gn = (grad / np.float32(24)).astype(np.float64) / (np.abs(back['grad_hist'][i]) + 1)
+                P = w.shape[1]
+                _row_close(out['obs'][i], np.concatenate([np.zeros(P), [out['obs'][i][P]], gn]),
+                           what='set_state order %s env %d' % (hidden, i))
         finally:
             eng.close()
 

@@ -132,6 +132,45 @@ def test_many_envs_against_live_oracle():
         eng.close()
 
 
+def test_config5_benchmark_size_sampled_envs():
+    """Config 5's per-GPU shard at its benchmark size (1024 envs x 4 agents,
+    func4, H = 5, max_batches = 400) with the bench's actions uniform(1, 3)
+    (learning rates 1e-3..1e-1: the loss > 1e4 early stop fires): envs 0, 1,
+    511, 512, 1022 and 1023 against live oracle runners over 48 steps."""
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    E, P, H, MB, T = 1024, 4, 5, 400, 48
+    sample = [0, 1, 511, 512, 1022, 1023]
+    actions = np.random.RandomState(7).uniform(1, 3, (T, E, P)).astype(np.float32)
+    eng = MultiOptEngine(E, 'func4', max_batches=MB, max_history=H)
+    refs = [OptEnvRunner(OracleMulti(P, max_batches=MB, max_history=H)) for _ in sample]
+    try:
+        first = eng.reset()
+        for e, r in zip(sample, refs):
+            assert np.array_equal(first[e * P:(e + 1) * P], np.stack(r.reset()))
+        early = 0
+        for t in range(T):
+            out = eng.step(actions[t])
+            eng_theta = eng.get_state()['theta']
+            for e, runner in zip(sample, refs):
+                states, rewards, dones, infos = runner.step(list(actions[t, e].reshape(P, 1)))
+                grad_abs = np.abs(runner._environment.history['gradients']).astype(np.float64)
+                if dones[0]:
+                    early += infos[0]['episode']['l'] < MB
+                    states = runner.reset()
+                rows = slice(e * P, (e + 1) * P)
+                what = (t, e)
+                assert np.all(out['done'][rows] == dones[0]), what
+                assert int(out['episode_len'][e]) == infos[0]['episode']['l'], what
+                _close_rows(out['obs'][rows], np.stack(states))
+                assert abs(out['reward'][e * P] - rewards[0]) <= 1e-6 * max(1.0, abs(rewards[0])), what
+                if not dones[0]:
+                    assert np.array_equal(eng_theta[e], runner._environment.model.params), what
+                _close_info(out['info'][e], _ref_info(infos[0]), grad_abs=grad_abs)
+        assert early > 0          # the loss > 1e4 branch was exercised
+    finally:
+        eng.close()
+
+
 def test_single_env_api_matches_oracle():
     from custom_envs_amd import make
     env = make('MultiOptLRs-v0', problem='func', max_batches=12)

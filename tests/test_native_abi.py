@@ -118,17 +118,21 @@ def test_native_mlp_seeding_against_live_numpy(seed):
 
 
 @pytest.mark.parametrize('change', [dict(n_classes=33), dict(n_layers=5),
-                                    dict(precision=_native.CE_F64)])
+                                    dict(precision=_native.CE_F64),
+                                    dict(n_layers=2, hidden=(300, 64, 0, 0))])
 def test_unsupported_mlp_shape_is_loud(change):
     """Networks the engine does not run (more than 32 classes, more than 4
-    hidden layers, float64) fail at ce_create before any HIP call; every
-    other width / depth / batch size runs (the fused config-3 kernel or the
-    layered path)."""
+    hidden layers, a hidden layer wider than 256 -- the forward keeps a
+    layer's activations in MFMA accumulators --, float64) fail at ce_create
+    before any HIP call; every other width / depth / batch size runs (the
+    fused config-3 kernel or the layered path)."""
     lib = _native.load()
     base = dict(abi_version=_native.ABI_VERSION, problem=_native.CE_PROBLEM_MLP,
                 precision=_native.CE_F32, num_envs=1, n_rows=128, n_features=16,
                 n_classes=10, batch_size=32, max_steps=40, n_hidden=64)
     base.update(change)
+    if 'hidden' in base:
+        base['hidden'] = (ctypes.c_int32 * 4)(*base['hidden'])
     cfg = _native.CeConfig(**base)
     x = np.zeros((128, base['n_features']))
     y = np.zeros(128, np.int32)
