@@ -18,9 +18,9 @@ launch) the ranks come from RANK/WORLD_SIZE.
 Multi-GPU (config 4).  Every step all-gathers the packed outputs of every
 rank (custom_envs_amd/distributed.py: ONE all_gather_into_tensor of the
 compact per-env record [obs without its identically-zero weight block |
-reward | objective | accuracy | episode_len] in 256-B-aligned segments,
-RCCL over xGMI; done is episode_len >= 40 and the full obs rows are
-rebuilt lazily on the consumer).  ``value`` is the SERIAL schedule: the
+objective | accuracy | episode_len], 96 B at P = 20, in 256-B-aligned
+segments, RCCL over xGMI; done is episode_len >= 40, reward is -objective
+(B = N) and the full obs rows are rebuilt lazily on the consumer).  ``value`` is the SERIAL schedule: the
 step kernel, then the collective, every step -- what a closed-loop learner
 consumes.  The line also carries ``value_gather_pipelined`` (two output
 buffers, the collective of step t on RCCL's stream while step t+1's kernel
@@ -145,6 +145,10 @@ def parse(argv=None):
                    help='launcher + rank protocol only (gloo on CPU, no engine)')
     p.add_argument('--profile-only', action='store_true',
                    help='run the timed steps only (for rocprofv3)')
+    p.add_argument('--measure-traffic', action='store_true',
+                   help='rank 0 at N = 1: measure roofline.traffic in this run (two rocprofv3 '
+                        '--pmc passes of this workload as child processes, scripts/traffic.py); '
+                        'default: the committed profiles/<round>_traffic_<workload>.json')
     args = p.parse_args(argv)
     args.hidden = tuple(int(h) for h in str(args.hidden).split(',') if h)
     if args.workload == 'mnist' and '--steps' not in (argv or sys.argv):
@@ -765,6 +769,8 @@ def main():
             line['gather_record'] = 'compact' if shard.compact else 'full'
             line['gather_mode'] = gather_mode
             line['gather_graph'] = gather_graph
+        bpe = line['roofline'].get('bytes_per_env_step')
+        line['roofline'].update(traffic_fields(args, eng, E, bpe if isinstance(bpe, (int, float)) else None))
         line['cpu_baseline'] = cpu
         if host_rate is not None:
             line['host_loop_env_steps_per_s'] = host_rate
@@ -810,17 +816,57 @@ def _common(args, world, E, S, elapsed, shard):
     }
 
 
-def _pmc_traffic(E, precision, kernel):
-    pmc_path = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
-    if not os.path.exists(pmc_path):
-        return None
-    with open(pmc_path) as fh:
-        pmc = json.load(fh)
-    entry = pmc.get(kernel) if isinstance(pmc.get(kernel), dict) else (
-        pmc if kernel == 'optimize' else {})
-    if entry.get('envs') == E and entry.get('precision') == precision:
-        return entry.get('hbm_bytes_per_launch')
-    return None
+# roofline.traffic: HBM bytes per step from rocprofv3 counters
+# (scripts/traffic.py).  The committed summaries of this round are named here
+# and reported in roofline.traffic_source; --measure-traffic takes them in
+# the run instead.
+TRAFFIC_ROUND = 'r04'
+TRAFFIC_MARKER = {'optimize': 'optimize_lr_mfma_kernel', 'multi': 'multi_step_kernel',
+                  'mlp': 'mlp_step_kernel', 'net': 'net_finish_kernel',
+                  'nn': 'nn_finalize_kernel', 'mnist': 'optimize_'}
+
+
+def _traffic_name(args, eng):
+    if args.workload == 'mlp':
+        return 'net' if eng.step_kernel.startswith('net<') else 'mlp'
+    return args.workload
+
+
+def _traffic_bench_args(args):
+    out = ['--workload', args.workload, '--envs', str(args.envs), '--profile-only',
+           '--steps', '6', '--warmup', '1', '--precision', args.precision,
+           '--batch-size', str(args.batch_size), '--hidden', ','.join(map(str, args.hidden))]
+    return out
+
+
+def traffic_fields(args, eng, E, bpe=None):
+    """{'traffic': bytes per step, 'traffic_source': where it came from}."""
+    name = _traffic_name(args, eng)
+    sys.path.insert(0, os.path.join(ROOT, 'scripts'))
+    import traffic as tr
+    if args.measure_traffic and int(os.environ.get('WORLD_SIZE', '1')) == 1:
+        try:
+            f, w = tr.collect(TRAFFIC_ROUND, name, _traffic_bench_args(args),
+                              os.path.join(ROOT, 'gpurun_out', 'traffic', name))
+            out, path = tr.summarize(f, w, TRAFFIC_MARKER[name], E, name, TRAFFIC_ROUND, bpe,
+                                     {'bench_args': ' '.join(_traffic_bench_args(args))})
+            return {'traffic': out['hbm_bytes_per_step'],
+                    'traffic_source': 'measured in this run: %s' % os.path.relpath(path, ROOT)}
+        except Exception as exc:      # the committed file, and say why
+            why = 'in-run measurement failed (%s); ' % str(exc)[:160]
+    else:
+        why = ''
+    path = os.path.join(ROOT, 'profiles', '%s_traffic_%s.json' % (TRAFFIC_ROUND, name))
+    if not os.path.exists(path):
+        return {'traffic': None, 'traffic_source': why + 'no %s' % os.path.relpath(path, ROOT)}
+    with open(path) as fh:
+        rec = json.load(fh)
+    if rec.get('envs') != E:
+        return {'traffic': None, 'traffic_source': why + '%s is for %s envs' % (
+            os.path.relpath(path, ROOT), rec.get('envs'))}
+    return {'traffic': rec['hbm_bytes_per_step'],
+            'traffic_source': why + '%s (round %s, %s)' % (os.path.relpath(path, ROOT), rec['round'],
+                                                          rec['bench_args'])}
 
 
 def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
@@ -847,7 +893,7 @@ def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, sh
         'roofline': {
             'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
             'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
-            'traffic': _pmc_traffic(E, args.precision, 'optimize'),
+            'traffic': None,
             'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
             'kernel_ms_mean': kernel_ms_mean,
             'kernel': 'ce::' + eng.step_kernel,
@@ -884,7 +930,7 @@ def multi_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard
         'roofline': {
             'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
             'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
-            'traffic': _pmc_traffic(E, 'f32', 'multi'),
+            'traffic': None,
             'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
             'kernel_ms_mean': kernel_ms_mean,
             'kernel': 'ce::multi_step_kernel<4>',

@@ -390,8 +390,10 @@ void copy_out(const ce_engine *e, const ce_outputs &src, const ce_outputs *dst) 
 
 // every output pointer set (the compact form may leave done null)
 bool complete(const ce_outputs *o, bool compact = false) {
-    return o && o->obs && o->reward && (o->done || compact) && o->objective && o->accuracy &&
-           o->episode_len;
+    // the compact form has no done (episode_len >= max_steps) and no reward
+    // (-objective: B = N)
+    return o && o->obs && (o->reward || compact) && (o->done || compact) && o->objective &&
+           o->accuracy && o->episode_len;
 }
 
 int do_step(ce_engine *e, const float *actions, const ce_outputs *out, uint32_t flags,

@@ -27,6 +27,12 @@ int dev_alloc(T **p, size_t count, bool zero = false) {
 
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
+// workgroups per env of the streaming kernels (each loops over its env's rows
+// / tasks): enough to fill the chip at a few hundred envs, few enough that
+// dispatch is not the bound
+constexpr int kNetUpdBlocks = 8;
+constexpr int kNetGradBlocks = 8;
+
 }  // namespace
 
 int net_geometry(int n_hidden, const int *dims, NetGeom *g) {
@@ -44,19 +50,27 @@ int net_geometry(int n_hidden, const int *dims, NetGeom *g) {
                                              "accumulators)");
     if (dims[nl] > kNetMaxClasses)
         return fail(CE_EUNSUPPORTED, "network: at most 32 classes");
+    // every hidden layer padded to one width (64 or 256 units): the forward
+    // is compiled per hidden-layer width (net_fwd_kernel<NCGH>); the output
+    // layer (K <= 32) has 64
+    int oph = 64;
+    for (int l = 1; l < nl; ++l) oph = std::max(oph, round_up(dims[l], 64) > 64 ? kNetMaxOp : 64);
     int64_t flat = 0, img = 0;
     int chunk = 0, row = 0, bias = 0;
     for (int l = 0; l < nl; ++l) {
         g->din[l] = dims[l];
         g->dout[l] = dims[l + 1];
-        g->op[l] = round_up(dims[l + 1], 64);
+        g->op[l] = l + 1 < nl ? oph : 64;
         g->nchunk[l] = l == 0 ? (dims[0] + kNetChunk - 1) / kNetChunk : g->op[l - 1] / kNetChunk;
         g->chunk0[l] = chunk;
         g->row0[l] = row;
         g->img_off[l] = img;
         g->bias_rel[l] = bias;
         g->flat_w[l] = flat;
-        chunk += g->nchunk[l];
+        // the forward's chunk sequence: every layer starts on an even chunk
+        // (static LDS slot per chunk parity, net_kernels.h); an odd layer-0
+        // count gets a padding chunk that is neither loaded nor multiplied
+        chunk += (g->nchunk[l] + 1) & ~1;
         row += g->nchunk[l] * kNetChunk;
         img += static_cast<int64_t>(g->nchunk[l]) * kNetChunk * g->op[l];
         bias += g->op[l];
@@ -192,8 +206,10 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
     }
     p->task0[nl] = task;
     p->tpe = task;
+    // a few long-lived workgroups per env: one per 16 rows made 85k tiny
+    // workgroups at 1024 envs, dispatch-bound (0.99 ms for 3.3 GB)
     const int rows = geo.row0[nl] + (geo.bias_total + 255) / 256;
-    p->upd_blocks = std::max(1, std::min(128, (rows + 15) / 16));
+    p->upd_blocks = std::max(1, std::min(kNetUpdBlocks, (rows + 15) / 16));
     CE_HIP(hipDeviceSynchronize());
     *out = p;
     return CE_OK;
@@ -274,7 +290,10 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         for (int l = 0; l < kNetL; ++l) f.act_mb[l] = p->act_mb[l];
         f.dz_out = p->dz_out;
         const unsigned grid = static_cast<unsigned>((E + 7) / 8 * 8) * p->T;
-        hipLaunchKernelGGL(net_fwd_kernel, dim3(grid), dim3(kNetThreads), 0, s, f);
+        if (g.op[0] == kNetMaxOp)
+            hipLaunchKernelGGL(net_fwd_kernel<kNetMaxOp / 64>, dim3(grid), dim3(kNetThreads), 0, s, f);
+        else
+            hipLaunchKernelGGL(net_fwd_kernel<1>, dim3(grid), dim3(kNetThreads), 0, s, f);
     }
     for (int lh = nl - 2; lh >= 0; --lh) {
         NetBwdArgs b{};
@@ -312,7 +331,7 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         r.step = a.step;
         r.G = a.G;
         r.obs = a.obs;
-        hipLaunchKernelGGL(net_grad_kernel, dim3(static_cast<unsigned>(E) * p->tpe), dim3(kNetThreads),
+        hipLaunchKernelGGL(net_grad_kernel, dim3(std::min(p->tpe, kNetGradBlocks), E), dim3(kNetThreads),
                            0, s, r);
     }
     hipLaunchKernelGGL(net_finish_kernel, dim3(E), dim3(kNetThreads), 0, s, fin_args(p, a));

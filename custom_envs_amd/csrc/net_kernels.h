@@ -70,30 +70,27 @@ struct NetUpdArgs {
 
 __global__ __launch_bounds__(kNetThreads) void net_update_kernel(NetUpdArgs a) {
     const int e = blockIdx.y;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (blockIdx.x == 0 && threadIdx.x == 0) a.step[e] += 1;
     float *img = a.img + static_cast<size_t>(e) * a.g.Pimg;
     const float *act = a.act + static_cast<size_t>(e) * a.P;
     const int nl = a.g.nl;
     const int rows_w = a.g.row0[nl];
-    const int rows = rows_w + a.g.bias_total / 256 + ((a.g.bias_total & 255) ? 1 : 0);
+    const int rows = rows_w + (a.g.bias_total + 255) / 256;
     constexpr int U = 4;                                    // rows in flight per wave
-    const int stride = gridDim.x * 4;
+    const int stride = gridDim.x * 4;                       // waves over this env
     for (int r0 = blockIdx.x * 4 + wave; r0 < rows; r0 += U * stride) {
         net_f4 w[U];
         float av[U][4];
         float *dst[U];
-        bool any[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int r = r0 + u * stride;
-            any[u] = false;
+            const int r = r0 + u * stride;                  // wave-uniform
             dst[u] = nullptr;
 #pragma unroll
             for (int q = 0; q < 4; ++q) av[u][q] = 0.0f;
             if (r >= rows) continue;
-            int64_t p0 = -1;           // flat index of column 4 lane (weights), per column (bias)
-            int64_t pb[4] = {-1, -1, -1, -1};
+            int64_t pb[4] = {-1, -1, -1, -1};               // flat index of each column
             if (r < rows_w) {
                 int l = 0;
                 while (l + 1 < nl && r >= a.g.row0[l + 1]) ++l;
@@ -101,7 +98,7 @@ __global__ __launch_bounds__(kNetThreads) void net_update_kernel(NetUpdArgs a) {
                 const int k = net_row_unit(l, q);
                 const int v = 4 * lane;
                 if (k < a.g.din[l] && v < a.g.dout[l]) {
-                    p0 = a.g.flat_w[l] + static_cast<int64_t>(k) * a.g.dout[l] + v;
+                    const int64_t p0 = a.g.flat_w[l] + static_cast<int64_t>(k) * a.g.dout[l] + v;
                     dst[u] = img + a.g.img_off[l] + static_cast<int64_t>(q) * a.g.op[l] + v;
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
@@ -122,14 +119,22 @@ __global__ __launch_bounds__(kNetThreads) void net_update_kernel(NetUpdArgs a) {
                 }
             }
             if (!dst[u]) continue;
-            any[u] = true;
             w[u] = *reinterpret_cast<const net_f4 *>(dst[u]);
+            if (pb[3] == pb[0] + 3 && ((reinterpret_cast<uintptr_t>(act + pb[0]) & 7) == 0)) {
+                const float2 lo = *reinterpret_cast<const float2 *>(act + pb[0]);
+                const float2 hi = *reinterpret_cast<const float2 *>(act + pb[0] + 2);
+                av[u][0] = lo.x;
+                av[u][1] = lo.y;
+                av[u][2] = hi.x;
+                av[u][3] = hi.y;
+            } else {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) av[u][c] = pb[c] >= 0 ? act[pb[c]] : 0.0f;
+                for (int c = 0; c < 4; ++c) av[u][c] = pb[c] >= 0 ? act[pb[c]] : 0.0f;
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (any[u])
+            if (dst[u])
                 *reinterpret_cast<net_f4 *>(dst[u]) =
                     net_f4{w[u][0] - av[u][0], w[u][1] - av[u][1], w[u][2] - av[u][2], w[u][3] - av[u][3]};
     }
@@ -142,8 +147,11 @@ __global__ __launch_bounds__(kNetThreads) void net_update_kernel(NetUpdArgs a) {
 // n = lane & 15, which is exactly the B operand layout of layer l + 1's
 // K steps (net_img_row), so the chain never leaves registers.  A operand:
 // the lane's 16-byte LDS read of weight row k, columns 64c + 4m .. +3 =
-// four output blocks (c, 0..3).  Weights arrive in 32-row chunks by LDS-DMA,
-// double-buffered; the chunk sequence runs across layer boundaries.
+// four output blocks (c, 0..3).  Weights stream through two LDS slots in
+// 32-row chunks, the chunk sequence running across layer boundaries: chunk
+// ci + 1 is loaded into registers while chunk ci is multiplied, and written
+// to the free slot after it (register staging: an LDS-DMA in flight makes
+// the compiler wait for it before every LDS read).
 struct NetFwdArgs {
     NetGeom g;
     int E, N, B, T, F16;
@@ -161,8 +169,139 @@ __device__ __forceinline__ net_f4 net_mfma16(float a, float b, net_f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Four K steps (half s of a 32-row chunk) into the NCG output groups (op =
+// 64 NCG): step b takes B operand bv[b]; its A operand is LDS row 16s + 4g + b
+// (layer 0: lane group g holds features 16t + 4g .. + 3 of the Xt image) or
+// 16s + 4b + g (hidden layers: chunk row rho = 16 (j & 1) + 4i + g).  The
+// reads of step b + 1 issue under step b's MFMAs; the empty asm keeps the
+// compiler from hoisting more (it would run out of registers).
+template <int NCG, bool L0>
+__device__ __forceinline__ void net_half_mm(const float *sl, int s, int g, int n, const net_f4 &bv,
+                                            net_f4 (&hout)[16]) {
+    constexpr int op = 64 * NCG;
+    net_f4 w[2][NCG];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        if (k < 4) {
+            const float *wr = sl + (16 * s + (L0 ? 4 * g + k : 4 * k + g)) * op + 4 * n;
+#pragma unroll
+            for (int c = 0; c < NCG; ++c) w[k & 1][c] = *reinterpret_cast<const net_f4 *>(wr + 64 * c);
+        }
+        if (k > 0) {
+            const int kk = k - 1;
+#pragma unroll
+            for (int c = 0; c < NCG; ++c)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    hout[c * 4 + j] = net_mfma16(w[kk & 1][c][j], bv[kk], hout[c * 4 + j]);
+        }
+        asm volatile("" ::: "memory");
+    }
+}
+
+// Per-workgroup state of the forward's weight stream.  The two slots are
+// DISTINCT __shared__ arrays and every access names one statically: the
+// compiler then knows an LDS-DMA in flight into one slot does not alias the
+// reads of the other, and inserts no vmcnt wait before them (with a runtime
+// slot index it waited for the DMA before every read).
+struct NetStream {
+    const NetGeom *geo;
+    const float *img;
+    int wave, lane, total;
+};
+
+// LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction) of chunk ci
+// into dst; a layer-0 padding chunk (layer 0 is padded to an even chunk
+// count, net_geometry) loads nothing
+__device__ __forceinline__ void net_issue(const NetStream &ws, int ci, float *dst) {
+    if (ci >= ws.total) return;
+    const NetGeom &g = *ws.geo;
+    int l = 0;
+    while (l + 1 < g.nl && ci >= g.chunk0[l + 1]) ++l;
+    const int lc = ci - g.chunk0[l];
+    if (lc >= g.nchunk[l]) return;
+    const int op = g.op[l];
+    const float *src = ws.img + g.img_off[l] + static_cast<int64_t>(lc) * kNetChunk * op;
+    const int ninst = op >> 3;
+    for (int k = ws.wave; k < ninst; k += kNetFwdWaves)
+        __builtin_amdgcn_global_load_lds(
+            (__attribute__((address_space(1))) void *)(src + k * 256 + ws.lane * 4),
+            (__attribute__((address_space(3))) void *)(dst + k * 256), 16, 0, 0);
+}
+
+// top of chunk ci: this wave's DMA (and X loads) of chunk ci landed, then the
+// workgroup's; the other slot is free for chunk ci + 1 (net_issue)
+// (the builtin, not inline asm: the compiler's wait tracking sees it and
+// knows the X operands loaded with the chunk are in, instead of waiting for
+// them again behind the next DMA -- vmcnt counts in order)
+__device__ __forceinline__ void net_chunk_wait() {
+    __builtin_amdgcn_s_waitcnt(0x0f70);                     // vmcnt(0), expcnt / lgkmcnt untouched
+    __syncthreads();
+}
+
+// Layer 0 over its chunks (padded to even): B operands from the Xt image,
+// prefetched a chunk ahead; slot A for even chunks, B for odd.
+template <int NCG>
+__device__ __forceinline__ void net_layer0(const NetStream &ws, int &ci, int nch, int F16,
+                                           const float *xt, int g, int n, float *sa, float *sb,
+                                           net_f4 (&hout)[16]) {
+    net_f4 xn[2];
+    auto xload = [&](int lc) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+            xn[t] = 2 * lc + t < F16 ? *reinterpret_cast<const net_f4 *>(xt + (2 * lc + t) * 256)
+                                     : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
+    };
+    xload(0);
+    // the X operands are copied out before the next DMA issues: vmcnt counts
+    // in order, so a later use would wait for that DMA as well
+    for (int lc = 0; lc < nch; lc += 2, ci += 2) {
+        net_chunk_wait();
+        net_f4 x0 = xn[0], x1 = xn[1];
+        net_issue(ws, ci + 1, sb);
+        if (lc + 1 < nch) xload(lc + 1);
+        net_half_mm<NCG, true>(sa, 0, g, n, x0, hout);
+        net_half_mm<NCG, true>(sa, 1, g, n, x1, hout);
+        net_chunk_wait();
+        x0 = xn[0];
+        x1 = xn[1];
+        net_issue(ws, ci + 2, sa);
+        if (lc + 1 < nch) {                                 // not the padding chunk
+            if (lc + 2 < nch) xload(lc + 2);
+            net_half_mm<NCG, true>(sb, 0, g, n, x0, hout);
+            net_half_mm<NCG, true>(sb, 1, g, n, x1, hout);
+        }
+    }
+}
+
+// A hidden-to-next layer over its nch (2 or 8) chunks: chunk lc holds the
+// units of input blocks (lc >> 1, 2 (lc & 1) + {0, 1}), B operands straight
+// from the previous layer's accumulators.  hin rotates down by four blocks
+// per chunk pair, so the loop keeps static register indices (fully unrolled
+// it spilled 4-28k VGPRs).
+template <int NCG>
+__device__ __forceinline__ void net_layer(const NetStream &ws, int &ci, int nch, int g, int n,
+                                          float *sa, float *sb, net_f4 (&hin)[16], net_f4 (&hout)[16]) {
+    for (int lc = 0; lc < nch; lc += 2, ci += 2) {
+        net_chunk_wait();
+        net_issue(ws, ci + 1, sb);
+        net_half_mm<NCG, false>(sa, 0, g, n, hin[0], hout);
+        net_half_mm<NCG, false>(sa, 1, g, n, hin[1], hout);
+        net_chunk_wait();
+        net_issue(ws, ci + 2, sa);
+        net_half_mm<NCG, false>(sb, 0, g, n, hin[2], hout);
+        net_half_mm<NCG, false>(sb, 1, g, n, hin[3], hout);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) hin[i] = hin[i + 4];
+    }
+}
+
+// NCGH: 64-unit output groups of every hidden layer (net_geometry pads all
+// hidden widths to one op: 64 or 256); the output layer has one (K <= 32).
+template <int NCGH>
 __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
-    __shared__ __attribute__((aligned(16))) float slot[2][kNetSlotFloats];
+    __shared__ __attribute__((aligned(16))) float slot_a[kNetSlotFloats];
+    __shared__ __attribute__((aligned(16))) float slot_b[kNetSlotFloats];
     __shared__ __attribute__((aligned(16))) float sbias[kNetMaxBias];
     __shared__ double red_loss[2][kNetFwdWaves];
     __shared__ int red_hits[2][kNetFwdWaves];
@@ -180,7 +319,7 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     const bool rvalid = row < a.N;
     const float *img = a.img + static_cast<size_t>(e) * a.g.Pimg;
     const int nl = a.g.nl;
-    const int total = a.g.chunk0[nl];
+    NetStream ws{&a.g, img, wave, lane, a.g.chunk0[nl]};
 
     for (int i = tid; i < a.g.bias_total; i += kNetThreads) sbias[i] = img[a.g.bias_base + i];
     int slot_n = -1;
@@ -189,29 +328,6 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
         slot_n = a.mb_slot ? a.mb_slot[static_cast<size_t>(e) * a.N + row] : row;
         yl = a.label[row];
     }
-
-    auto issue = [&](int ci) {                              // LDS-DMA of chunk ci
-        int l = 0;
-        while (l + 1 < nl && ci >= a.g.chunk0[l + 1]) ++l;
-        const int op = a.g.op[l];
-        const float *src = img + a.g.img_off[l] + static_cast<int64_t>(ci - a.g.chunk0[l]) * kNetChunk * op;
-        float *dst = &slot[ci & 1][0];
-        const int ninst = op >> 3;                          // 1 KB per wave instruction
-        for (int k = wave; k < ninst; k += kNetFwdWaves)
-            __builtin_amdgcn_global_load_lds(
-                (__attribute__((address_space(1))) void *)(src + k * 256 + lane * 4),
-                (__attribute__((address_space(3))) void *)(dst + k * 256), 16, 0, 0);
-    };
-    const int rb = tile * (kNetTile / 16) + wave;           // this wave's 16-row block of Xt
-    auto xload = [&](int lc, net_f4 *xv) {                  // layer-0 B operands of chunk lc
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int tg = 2 * lc + t;
-            xv[t] = tg < a.F16 ? *reinterpret_cast<const net_f4 *>(
-                                     a.Xt + ((static_cast<size_t>(rb) * a.F16 + tg) * 64 + lane) * 4)
-                               : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-    };
 
     net_f4 hin[16], hout[16];
     auto bias_init = [&](int l) {
@@ -225,85 +341,24 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
                                           : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
     };
 
-    net_f4 xc[2], xn[2];
-    issue(0);
-    xload(0, xn);
+    net_issue(ws, 0, slot_a);
     __syncthreads();                                        // sbias
     bias_init(0);
     int ci = 0;
 
     // ---- layer 0: K = the input features, B operand = X rows
-    {
-        const int op = a.g.op[0], ncg = op >> 6, nch = a.g.nchunk[0];
-        for (int lc = 0; lc < nch; ++lc, ++ci) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own DMA + X of chunk ci
-            __syncthreads();                                   // all of chunk ci; slot ci+1 free
-            if (ci + 1 < total) issue(ci + 1);
-            xc[0] = xn[0];
-            xc[1] = xn[1];
-            if (lc + 1 < nch) xload(lc + 1, xn);
-            const float *sl = &slot[ci & 1][0];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                if (2 * lc + t < a.F16) {                   // wave-uniform
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float bx = xc[t][q];
-                        const float *wr = sl + (16 * t + 4 * g + q) * op + 4 * n;
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            if (c < ncg) {
-                                const net_f4 w4 = *reinterpret_cast<const net_f4 *>(wr + 64 * c);
-#pragma unroll
-                                for (int j = 0; j < 4; ++j)
-                                    hout[c * 4 + j] = net_mfma16(w4[j], bx, hout[c * 4 + j]);
-                            }
-                        }
-                    }
-                }
-            }
-        }
-    }
+    // (this wave's 16-row block of Xt, the lane's float4 of feature group 0)
+    net_layer0<NCGH>(ws, ci, a.g.nchunk[0], a.F16,
+                     a.Xt + (static_cast<size_t>(tile * (kNetTile / 16) + wave) * a.F16 * 64 + lane) * 4,
+                     g, n, slot_a, slot_b, hout);
 
     // ---- layers 1 .. nl-1: K = the previous layer's units, from registers
-    for (int l = 0; l < nl; ++l) {
-        if (l > 0) {
-            const int op = a.g.op[l], ncg = op >> 6, nch = a.g.nchunk[l];
-#pragma unroll
-            for (int lc = 0; lc < 2 * 4; ++lc) {
-                if (lc < nch) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __syncthreads();
-                    if (ci + 1 < total) issue(ci + 1);
-                    const float *sl = &slot[ci & 1][0];
-                    const int cin = lc >> 1, jj = lc & 1;
-#pragma unroll
-                    for (int jl = 0; jl < 2; ++jl) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const float bx = hin[cin * 4 + 2 * jj + jl][i];
-                            const float *wr = sl + (16 * jl + 4 * i + g) * op + 4 * n;
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) {
-                                if (c < ncg) {
-                                    const net_f4 w4 = *reinterpret_cast<const net_f4 *>(wr + 64 * c);
-#pragma unroll
-                                    for (int j = 0; j < 4; ++j)
-                                        hout[c * 4 + j] = net_mfma16(w4[j], bx, hout[c * 4 + j]);
-                                }
-                            }
-                        }
-                    }
-                    ++ci;
-                }
-            }
-        }
-        if (l + 1 == nl) break;
+    for (int l = 0; l + 1 < nl; ++l) {
         // hidden layer l done: relu (optimize_nn.py: Dense(relu)), the
         // minibatch rows' activations out, next layer's bias in the accumulators
-        const int op = a.g.op[l], ncg = op >> 6;
+        const int op = a.g.op[l];
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < NCGH; ++c)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -311,15 +366,16 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
         if (slot_n >= 0) {
             float *dst = a.act_mb[l] + (static_cast<size_t>(e) * a.B + slot_n) * op;
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (c < ncg)
+            for (int c = 0; c < NCGH; ++c)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        *reinterpret_cast<net_f4 *>(dst + 64 * c + 16 * g + 4 * i) =
-                            net_f4{hin[c * 4 + 0][i], hin[c * 4 + 1][i], hin[c * 4 + 2][i], hin[c * 4 + 3][i]};
+                for (int i = 0; i < 4; ++i)
+                    *reinterpret_cast<net_f4 *>(dst + 64 * c + 16 * g + 4 * i) =
+                        net_f4{hin[c * 4 + 0][i], hin[c * 4 + 1][i], hin[c * 4 + 2][i], hin[c * 4 + 3][i]};
         }
         bias_init(l + 1);
+        if (l + 2 < nl) net_layer<NCGH>(ws, ci, a.g.nchunk[l + 1], g, n, slot_a, slot_b, hin, hout);
     }
+    net_layer<1>(ws, ci, a.g.nchunk[nl - 1], g, n, slot_a, slot_b, hin, hout);   // the output layer
 
     // ---- logits -> softmax (utils_math.py:51-63), -log(p_y + 1e-16)
     // (utils_math.py:25-34), np.argmax's first maximum of P; class 16g + 4i + j
@@ -478,84 +534,96 @@ __device__ __forceinline__ net_f16 net_mfma32(float a, float b, net_f16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// K steps of the [dW; db] product loaded in one batch (their loads in flight
+// together, then the MFMAs)
+constexpr int kNetGradBatch = 16;
+
 __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
-    const int e = blockIdx.x / a.tpe;
-    const int task = blockIdx.x - e * a.tpe;
+    const int e = blockIdx.y;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, h = lane >> 5, m = lane & 31;
     const int nl = a.g.nl;
-    int l = 0;
-    while (l + 1 < nl && task >= a.task0[l + 1]) ++l;
-    const int tl = task - a.task0[l];
-    const int kt = tl / a.ut[l], ut = tl - kt * a.ut[l];
-    const int din = a.g.din[l], dout = a.g.dout[l];
-    const int u0 = ut * 256 + 64 * wave;
-    if (u0 >= dout) return;                                 // no barriers in this kernel
-    const int k0 = kt * 32, k = k0 + m;
-    // A: [H_{l-1} | 1] rows (layer 0: the dataset rows of sequence[0])
-    const float *Hin = nullptr;
-    int hstride = 0;
-    const int32_t *rows = nullptr;
-    if (l == 0) {
-        if (a.order)
-            rows = a.order + (static_cast<size_t>(a.order_sel[e]) * a.E + e) * a.N;
-    } else {
-        hstride = a.g.op[l - 1];
-        Hin = a.act_mb[l - 1] + static_cast<size_t>(e) * a.B * hstride;
-    }
-    const int opl = a.g.op[l];
-    const float *dz = (l + 1 == nl ? a.dz_out : a.dz_mb[l]) + static_cast<size_t>(e) * a.B * opl + u0 + m;
-    net_f16 acc0 = {}, acc1 = {};
-    const int steps = (a.B + 1) >> 1;
-    for (int s = 0; s < steps; ++s) {
-        const int r = 2 * s + h;
-        float xa = 0.0f, b0 = 0.0f, b1 = 0.0f;
-        if (r < a.B) {
-            if (k < din) {
-                if (l == 0) {
-                    const int xr = rows ? rows[r] : r;
-                    xa = a.X[static_cast<size_t>(xr) * a.F + k];
-                } else {
-                    xa = Hin[static_cast<size_t>(r) * hstride + k];
-                }
-            } else if (k == din) {
-                xa = 1.0f;                                  // the bias row
-            }
-            b0 = dz[static_cast<size_t>(r) * opl];
-            b1 = dz[static_cast<size_t>(r) * opl + 32];
-        }
-        acc0 = net_mfma32(xa, b0, acc0);
-        acc1 = net_mfma32(xa, b1, acc1);
-    }
-    // epilogue: accumulator r of lane (h, m) = row k0 + 8(r>>2) + 4h + (r&3) of
-    // [dW; db], unit u0 + 32 bb + m
     const int cur = a.step[e];
     const bool wipe = cur >= a.max_steps && a.auto_reset;
     const float fB = static_cast<float>(a.B);
     const size_t P = a.P;
     double *G = a.G + static_cast<size_t>(e) * P;
     float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
-    const int64_t fw = a.g.flat_w[l];
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb) {
-        const int u = u0 + 32 * bb + m;
-        const net_f16 &acc = bb ? acc1 : acc0;
-        double gold[16];
-        int64_t pp[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int kk = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
-            pp[r] = (kk <= din && u < dout) ? fw + static_cast<int64_t>(kk) * dout + u : -1;
-            gold[r] = pp[r] >= 0 ? G[pp[r]] : 0.0;
+    const int32_t *rows = a.order ? a.order + (static_cast<size_t>(a.order_sel[e]) * a.E + e) * a.N : nullptr;
+    for (int task = blockIdx.x; task < a.tpe; task += gridDim.x) {
+        int l = 0;
+        while (l + 1 < nl && task >= a.task0[l + 1]) ++l;
+        const int tl = task - a.task0[l];
+        const int kt = tl / a.ut[l], ut = tl - kt * a.ut[l];
+        const int din = a.g.din[l], dout = a.g.dout[l];
+        const int u0 = ut * 256 + 64 * wave;
+        if (u0 >= dout) continue;                           // wave-uniform; no barriers here
+        const int k0 = kt * 32, k = k0 + m;
+        // A: [H_{l-1} | 1] rows (layer 0: the dataset rows of sequence[0])
+        const float *Hin = nullptr;
+        int hstride = 0;
+        if (l > 0) {
+            hstride = a.g.op[l - 1];
+            Hin = a.act_mb[l - 1] + static_cast<size_t>(e) * a.B * hstride;
         }
+        const int opl = a.g.op[l];
+        const float *dz = (l + 1 == nl ? a.dz_out : a.dz_mb[l]) + static_cast<size_t>(e) * a.B * opl + u0 + m;
+        net_f16 acc0 = {}, acc1 = {};
+        const int steps = (a.B + 1) >> 1;
+        for (int s0 = 0; s0 < steps; s0 += kNetGradBatch) {
+            float xa[kNetGradBatch], b0[kNetGradBatch], b1[kNetGradBatch];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (pp[r] < 0) continue;
-            const float gv = acc[r] / fB;
-            const double gn = static_cast<double>(gv) / (fabs(gold[r]) + 1.0);
-            obs[pp[r]] = 0.0f;                              // wght_hist is identically 0
-            obs[P + 1 + pp[r]] = wipe ? 0.0f : static_cast<float>(gn);
-            G[pp[r]] = wipe ? 0.0 : gn;
+            for (int q = 0; q < kNetGradBatch; ++q) {
+                const int r = 2 * (s0 + q) + h;
+                xa[q] = 0.0f;
+                b0[q] = 0.0f;
+                b1[q] = 0.0f;
+                if (r < a.B) {
+                    if (k < din) {
+                        if (l == 0) {
+                            const int xr = rows ? rows[r] : r;
+                            xa[q] = a.X[static_cast<size_t>(xr) * a.F + k];
+                        } else {
+                            xa[q] = Hin[static_cast<size_t>(r) * hstride + k];
+                        }
+                    } else if (k == din) {
+                        xa[q] = 1.0f;                       // the bias row
+                    }
+                    b0[q] = dz[static_cast<size_t>(r) * opl];
+                    b1[q] = dz[static_cast<size_t>(r) * opl + 32];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kNetGradBatch; ++q) {
+                acc0 = net_mfma32(xa[q], b0[q], acc0);
+                acc1 = net_mfma32(xa[q], b1[q], acc1);
+            }
+        }
+        // epilogue: accumulator r of lane (h, m) = row k0 + 8(r>>2) + 4h + (r&3)
+        // of [dW; db], unit u0 + 32 bb + m; every G load of a block in flight
+        // before its stores
+        const int64_t fw = a.g.flat_w[l];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int u = u0 + 32 * bb + m;
+            const net_f16 &acc = bb ? acc1 : acc0;
+            double gold[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int kk = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
+                gold[r] = (kk <= din && u < dout) ? G[fw + static_cast<int64_t>(kk) * dout + u] : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int kk = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
+                if (kk > din || u >= dout) continue;
+                const int64_t p = fw + static_cast<int64_t>(kk) * dout + u;
+                const float gv = acc[r] / fB;
+                const double gn = static_cast<double>(gv) / (fabs(gold[r]) + 1.0);
+                obs[p] = 0.0f;                              // wght_hist is identically 0
+                obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(gn);
+                G[p] = wipe ? 0.0 : gn;
+            }
         }
     }
 }

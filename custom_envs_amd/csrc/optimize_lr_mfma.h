@@ -558,7 +558,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
 
     // ---- epilogue: the scalar and the parameter roles run side by side
 #if defined(CE_LR_EXP) && (CE_LR_EXP == 2 || CE_LR_EXP == 3)
-    if (srole) a.reward[es] = static_cast<float>(red_l[0][sj]);
+    if (srole && a.reward) a.reward[es] = static_cast<float>(red_l[0][sj]);
     return;                                             // experiment: no epilogue
 #endif
     if (srole) {
@@ -572,7 +572,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
         const double acc = div_rcp(ht, dB, rB);
         const double lnew = div_rcp(loss - lprev, dL, rL);
         const bool wipe = cur >= a.max_steps && a.auto_reset;
-        lr_store(&a.reward[es], static_cast<float>(-loss));
+        if (a.reward) lr_store(&a.reward[es], static_cast<float>(-loss));   // compact: -objective
         lr_store(&a.objective[es], static_cast<float>(loss));   // B == N: the same numbers
         lr_store(&a.accuracy[es], static_cast<float>(acc));
         lr_store(&a.obs[es * OS + P - OL], wipe ? 0.0f : static_cast<float>(lnew));

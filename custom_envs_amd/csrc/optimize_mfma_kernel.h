@@ -208,13 +208,15 @@ __global__ __launch_bounds__(kWave *kGenResetWaves) void optimize_reset_rt_kerne
     for (int i = lane; i < a.obs_stride; i += kWave) obs[i] = 0.0f;
 }
 
-// Z^T = sum over k of W'^T_k X^T_k as kGenChains independent accumulator
-// chains (a dependent f64 MFMA waits out the previous one's latency; two
-// chains keep the matrix pipe issuing), added at the end.
+// Z^T = sum over k of W'^T_k X^T_k as kGenChains accumulator chains, added
+// at the end.  One chain: the class-concatenated kernel
+// (optimize_cat_kernel.h) sums its forward in one chain too, and the two
+// kernels' results agree bit for bit (test_class_concatenated_agrees_with_
+// per_env_kernel); CE_GEN_CHAINS=2 builds the two-chain A/B arm.
 #ifdef CE_GEN_CHAINS
 constexpr int kGenChains = CE_GEN_CHAINS;
 #else
-constexpr int kGenChains = 2;
+constexpr int kGenChains = 1;
 #endif
 template <int NK>
 __device__ __forceinline__ gen_d4 gen_forward(const double (&wb)[NK], const double (&av)[NK]) {

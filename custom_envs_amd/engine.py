@@ -44,7 +44,10 @@ def _view(ptr, count, ctype, dtype, shape):
 
 
 def compact_derived(n_params, max_steps):
-    """The full obs rows and the done flags from the compact fields."""
+    """The full obs rows, the done flags and the reward from the compact
+    fields.  reward = -loss and objective = loss in the reference when B = N
+    (optimize.py:91,94-97: the full-data pass IS the minibatch), and
+    float32(-x) = -float32(x), so -objective is the reward bit for bit."""
     import torch
 
     def obs(f):
@@ -56,7 +59,10 @@ def compact_derived(n_params, max_steps):
     def done(f):
         return (f['episode_len'] >= max_steps).to(torch.uint8)
 
-    return {'obs': obs, 'done': done}
+    def reward(f):
+        return -f['objective']
+
+    return {'obs': obs, 'done': done, 'reward': reward}
 
 
 class OptimizeEngine:
@@ -168,7 +174,8 @@ class OptimizeEngine:
     @staticmethod
     def _outputs(out):
         obs = out['obs_tail'] if 'obs_tail' in out else out['obs']
-        return CeOutputs(obs=obs.data_ptr(), reward=out['reward'].data_ptr(),
+        return CeOutputs(obs=obs.data_ptr(),
+                         reward=out['reward'].data_ptr() if 'reward' in out else None,
                          done=out['done'].data_ptr() if 'done' in out else None,
                          objective=out['objective'].data_ptr(),
                          accuracy=out['accuracy'].data_ptr(),
@@ -177,8 +184,9 @@ class OptimizeEngine:
     def set_compact_outputs(self, on=True):
         """Device-pointer calls write the compact form (``ce_set_compact_outputs``):
         ``obs_tail`` = obs[:, P:] (the wght_hist block obs[:, :P] is
-        identically 0, optimize.py:84-86) and no ``done`` (done == episode_len
-        >= max_steps).  ``derived_fields`` rebuilds both.  Raises
+        identically 0, optimize.py:84-86), no ``done`` (done == episode_len
+        >= max_steps) and no ``reward`` (= -objective when B = N):
+        96 B per env at P = 20.  ``derived_fields`` rebuilds all three.  Raises
         ``NativeEngineError`` (CE_EUNSUPPORTED) unless this engine runs the
         two-class full-batch float64 kernel."""
         check(self._lib.ce_set_compact_outputs(self._h, 1 if on else 0), 'ce_set_compact_outputs')
@@ -190,7 +198,6 @@ class OptimizeEngine:
         import torch
         if self.compact:
             return [('obs_tail', torch.float32, 1, (self.act_dim + 1,)),
-                    ('reward', torch.float32, 1, ()),
                     ('objective', torch.float32, 1, ()),
                     ('accuracy', torch.float32, 1, ()),
                     ('episode_len', torch.int32, 1, ())]

@@ -16,4 +16,5 @@ tail -1 $OUT/bench_net.log | cut -c1-400; fatal $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_net -o run --output-format csv -- python3 bench.py --workload mlp --hidden 256,256 --batch-size 32 --envs 1024 --profile-only --steps 5 --warmup 1 > $OUT/prof_net.log 2>&1; rc=$?
 echo "prof rc=$rc"; fatal $rc
 find $OUT/prof_net -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-200 | head -20
+[ -n "${PMC:-}" ] && { OUT=$OUT/pmc bash scripts/gpu_pmc_net.sh || exit $?; }
 echo ALL_OK
