@@ -15,7 +15,7 @@ if os.environ.get('CE_LIB') == 'diag':
 elif os.environ.get('CE_LIB'):
     LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd_%s.so' % os.environ['CE_LIB'])
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 CE_OK, CE_EINVAL, CE_EHIP, CE_ENOMEM, CE_ESTATE, CE_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
 CE_PROBLEM_SOFTMAX, CE_PROBLEM_MLP = 0, 1
 CE_F64, CE_F32 = 0, 1
@@ -42,7 +42,7 @@ EXPORTS = (
 )
 
 CE_FUNC_ROSENBROCK_PAIRS = 0
-CE_MULTI_MAX_PARAMS = 16
+CE_MULTI_MAX_PARAMS = 64
 MULTI_INFO_KEYS = ('loss', 'batch_loss', 'weights_mean', 'weights_sum', 'actions_mean',
                    'actions_std', 'states_mean', 'states_sum', 'grads_mean', 'grads_sum',
                    'loss_mean', 'adjusted_loss', 'adjusted_grad', 'grad_diff')
@@ -68,7 +68,7 @@ class CeOutputs(ctypes.Structure):
 class CeMultiConfig(ctypes.Structure):
     _fields_ = [(name, ctypes.c_int32) for name in (
         'abi_version', 'device', 'num_envs', 'n_params', 'function', 'max_history',
-        'max_batches', 'auto_reset')] + [('initial_points', ctypes.c_float * 16)]
+        'max_batches', 'auto_reset')] + [('initial_points', ctypes.c_float * CE_MULTI_MAX_PARAMS)]
 
 
 class CeMultiOutputs(ctypes.Structure):

@@ -100,17 +100,22 @@ struct MlpStamps {
 };
 
 // LDS of the two phases of one env's step.
+// W2 rows are kMlpW2S = 17 floats apart: the dz1 = dz2 W2^T loop reads
+// w2s[j][k] with j across the lanes, and the 16-float stride put a 32-lane
+// group on 2 banks (16-way conflicts: 41.1 M conflict cycles per 4096-env
+// dispatch, profiles/r03_mlp_pmc.json "train")
+constexpr int kMlpW2S = kMlpMaxK + 1;
 struct MlpTrainShared {
     float part[4][kMlpHidden][kMlpBatch];     // per-wave partial H^T
     float hs[kMlpBatch][kMlpHidden + 1];      // H, then dz1 (sample-major)
-    float w2s[kMlpHidden][kMlpMaxK];
+    float w2s[kMlpHidden][kMlpW2S];
     float b1s[kMlpHidden], b2s[kMlpMaxK];
     float dz2[kMlpBatch][kMlpMaxK];
     float ce[kMlpBatch];
     int rows[kMlpBatch];
 };
 struct MlpInfoShared {
-    float w2s[kMlpHidden][kMlpMaxK];
+    float w2s[kMlpHidden][kMlpW2S];
     float b1s[kMlpHidden], b2s[kMlpMaxK];
     float red_loss[4];
     int red_hits[4];

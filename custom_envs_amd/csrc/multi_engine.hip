@@ -53,10 +53,13 @@ struct MultiEntry {
     MultiFn step, reset;
 };
 
+// every even dimension count up to CE_MULTI_MAX_PARAMS (one lane per agent:
+// an env's agents are a group of 2..64 lanes of one wave)
 #define CE_MULTI_ENTRY(P) {P, launch_multi_step<P>, launch_multi_reset<P>},
-const MultiEntry kMulti[] = {CE_MULTI_ENTRY(2) CE_MULTI_ENTRY(4) CE_MULTI_ENTRY(6)
-                                 CE_MULTI_ENTRY(8) CE_MULTI_ENTRY(10) CE_MULTI_ENTRY(12)
-                                     CE_MULTI_ENTRY(16)};
+#define CE_MULTI_ENTRY8(P) CE_MULTI_ENTRY(P) CE_MULTI_ENTRY(P + 2) CE_MULTI_ENTRY(P + 4) CE_MULTI_ENTRY(P + 6)
+const MultiEntry kMulti[] = {CE_MULTI_ENTRY8(2) CE_MULTI_ENTRY8(10) CE_MULTI_ENTRY8(18)
+                                 CE_MULTI_ENTRY8(26) CE_MULTI_ENTRY8(34) CE_MULTI_ENTRY8(42)
+                                     CE_MULTI_ENTRY8(50) CE_MULTI_ENTRY8(58)};
 
 }  // namespace
 

@@ -46,7 +46,7 @@ constexpr int kRawHist = 5;
 // up front, so CU-local load throughput matters).
 constexpr int kMultiBlock = 64 * CE_MULTI_WAVES;
 constexpr int kMultiInfo = 14;     // info keys, order in include/custom_envs_amd.h
-constexpr int kMultiMaxP = 16;
+constexpr int kMultiMaxP = 64;
 constexpr int kMultiStageH = 20;   // LDS-staged observation rows up to this H
 
 struct MultiArgs {
@@ -92,7 +92,7 @@ __device__ __forceinline__ const T &at32(const T *base, unsigned idx) {
 
 template <int P>
 struct Group {
-    static constexpr int G = P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : 16;
+    static constexpr int G = P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : P <= 16 ? 16 : P <= 32 ? 32 : 64;
 };
 
 // Sum over a group of G lanes by an xor butterfly on DPP / ds_swizzle

@@ -217,8 +217,10 @@ __device__ __forceinline__ unsigned xchg_u32(unsigned v) {
         return __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
     else if constexpr (OFF == 4)
         return __builtin_amdgcn_ds_swizzle(v, 0x101f);                      // xor 4 (bitmask mode)
-    else
+    else if constexpr (OFF == 8)
         return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xf, 0xf, false);  // row_ror:8 = xor 8
+    else                                                                     // 16, 32: ds_bpermute
+        return static_cast<unsigned>(__shfl_xor(static_cast<int>(v), OFF));
 }
 
 template <int OFF>

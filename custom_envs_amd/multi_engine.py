@@ -59,6 +59,10 @@ class MultiOptEngine:
                  initial_points=None, device=0, auto_reset=True):
         lib = _native.load()
         ndims, start = resolve_problem(problem, initial_points)
+        if ndims > _native.CE_MULTI_MAX_PARAMS:
+            raise ValueError('MultiOptLRs function problems run up to %d dimensions (one lane per '
+                             'agent, an env within one wave); got %d'
+                             % (_native.CE_MULTI_MAX_PARAMS, ndims))
         self.num_envs, self.n_params = int(num_envs), ndims
         self.max_history, self.max_batches = int(max_history), int(max_batches)
         cfg = CeMultiConfig(abi_version=_native.ABI_VERSION, device=int(device),

@@ -79,7 +79,7 @@
 extern "C" {
 #endif
 
-#define CE_ABI_VERSION 3
+#define CE_ABI_VERSION 4
 
 typedef struct ce_engine ce_engine;
 
@@ -219,7 +219,7 @@ int ce_set_state(ce_engine *eng, const ce_state *st);
  */
 typedef struct ce_multi_engine ce_multi_engine;
 
-#define CE_MULTI_MAX_PARAMS 16
+#define CE_MULTI_MAX_PARAMS 64
 
 typedef enum ce_function {
     /* sum of Rosenbrock 100(y - x^2)^2 + (1 - x)^2 over coordinate pairs

@@ -199,26 +199,49 @@ def test_single_env_api_matches_oracle():
         env.close()
 
 
-def test_many_agents_row_order():
-    """P = 12: sorted names put 'parameter-10' before 'parameter-2'."""
+@pytest.mark.parametrize('P', [12, 24, 38, 64])
+def test_many_agents_row_order(P):
+    """P = 12: sorted names put 'parameter-10' before 'parameter-2'; 24, 38
+    and 64 dimensions (OptimizeFunction takes any ndims, optimize_function.py:
+    20-40) run on 32- and 64-lane agent groups; theta, done, obs, reward
+    and info against the oracle across an early stop and max_batches."""
     from custom_envs_amd.multi_engine import MultiOptEngine
-    P = 12
     start = list(np.linspace(-1.5, 1.5, P))
-    eng = MultiOptEngine(2, {'ndims': P, 'initial_points': start}, max_batches=50)
-    ref = [OptEnvRunner(OracleMulti(P, initial_points=start, max_batches=50)) for _ in range(2)]
+    E = 3
+    eng = MultiOptEngine(E, {'ndims': P, 'initial_points': start}, max_batches=12)
+    ref = [OptEnvRunner(OracleMulti(P, initial_points=start, max_batches=12)) for _ in range(E)]
     try:
-        eng.reset()
-        for r in ref:
-            r.reset()
+        first = eng.reset()
+        assert np.array_equal(first, np.concatenate([np.stack(r.reset()) for r in ref]))
         rs = np.random.RandomState(5)
-        for t in range(8):
-            acts = rs.uniform(-1, 0.5, (2, P)).astype(np.float32)
+        for t in range(20):
+            acts = rs.uniform(-1, 0.5 + 1.5 * (t > 14), (E, P)).astype(np.float32)
             out = eng.step(acts)
-            for e in range(2):
-                states, _, _, _ = ref[e].step(list(acts[e].reshape(P, 1)))
-                _close_rows(out['obs'][e * P:(e + 1) * P], np.stack(states))
+            theta = eng.get_state()['theta']
+            for e in range(E):
+                states, rewards, dones, infos = ref[e].step(list(acts[e].reshape(P, 1)))
+                grad_abs = np.abs(ref[e]._environment.history['gradients']).astype(np.float64)
+                if dones[0]:
+                    states = ref[e].reset()
+                rows = slice(e * P, (e + 1) * P)
+                assert np.all(out['done'][rows] == dones[0]), (t, e)
+                assert int(out['episode_len'][e]) == infos[0]['episode']['l']
+                _close_rows(out['obs'][rows], np.stack(states))
+                assert abs(out['reward'][e * P] - rewards[0]) <= 1e-6 * max(1.0, abs(rewards[0]))
+                if not dones[0]:
+                    assert np.array_equal(theta[e], ref[e]._environment.model.params), (t, e)
+                _close_info(out['info'][e], _ref_info(infos[0]), grad_abs=grad_abs)
     finally:
         eng.close()
+
+
+def test_parameter_cap_is_loud():
+    from custom_envs_amd._native import CE_MULTI_MAX_PARAMS, NativeEngineError
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    assert CE_MULTI_MAX_PARAMS == 64
+    P = CE_MULTI_MAX_PARAMS + 2
+    with pytest.raises((NativeEngineError, ValueError)):
+        MultiOptEngine(1, {'ndims': P, 'initial_points': [0.5] * P})
 
 
 def test_optvecenv_monitor_pattern(tmp_path):
