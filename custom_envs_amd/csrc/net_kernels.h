@@ -68,75 +68,71 @@ struct NetUpdArgs {
     int32_t *step;
 };
 
+// One layer's rows [0, rows) of the image: row q holds input unit
+// net_row_unit(l, q); lane c4 updates columns 4 lane .. + 3 (U rows in
+// flight per wave).  The layer index is a compile-time constant at every
+// call, so its geometry comes from scalar registers, not memory.
+template <int U>
+__device__ __forceinline__ void net_update_rows(float *img_l, const float *act_l, int l, int rows,
+                                               int din, int dout, int op, int r0, int stride,
+                                               int lane) {
+    const int v = 4 * lane;
+    const bool vin = v < dout;
+    for (int r = r0; r < rows; r += U * stride) {
+        net_f4 w[U];
+        float av[U][4];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = r + u * stride;                   // wave-uniform
+            const int k = net_row_unit(l, q < rows ? q : 0);
+            ok[u] = q < rows && k < din && vin;
+            const int qc = ok[u] ? q : 0, kc = ok[u] ? k : 0, vc = vin ? v : 0;
+            w[u] = *reinterpret_cast<const net_f4 *>(img_l + static_cast<int64_t>(qc) * op + vc);
+            const float *ar = act_l + static_cast<int64_t>(kc) * dout + vc;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) av[u][c] = v + c < dout ? ar[c] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (ok[u])
+                *reinterpret_cast<net_f4 *>(img_l + static_cast<int64_t>(r + u * stride) * op + v) =
+                    net_f4{w[u][0] - av[u][0], w[u][1] - av[u][1], w[u][2] - av[u][2], w[u][3] - av[u][3]};
+    }
+}
+
 __global__ __launch_bounds__(kNetThreads) void net_update_kernel(NetUpdArgs a) {
     const int e = blockIdx.y;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (blockIdx.x == 0 && threadIdx.x == 0) a.step[e] += 1;
     float *img = a.img + static_cast<size_t>(e) * a.g.Pimg;
     const float *act = a.act + static_cast<size_t>(e) * a.P;
-    const int nl = a.g.nl;
-    const int rows_w = a.g.row0[nl];
-    const int rows = rows_w + (a.g.bias_total + 255) / 256;
-    constexpr int U = 4;                                    // rows in flight per wave
     const int stride = gridDim.x * 4;                       // waves over this env
-    for (int r0 = blockIdx.x * 4 + wave; r0 < rows; r0 += U * stride) {
-        net_f4 w[U];
-        float av[U][4];
-        float *dst[U];
+    const int r0 = blockIdx.x * 4 + wave;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int r = r0 + u * stride;                  // wave-uniform
-            dst[u] = nullptr;
+    for (int l = 0; l < kNetL; ++l) {
+        if (l >= a.g.nl) break;
+        net_update_rows<4>(img + a.g.img_off[l], act + a.g.flat_w[l], l, a.g.nchunk[l] * kNetChunk,
+                           a.g.din[l], a.g.dout[l], a.g.op[l], r0, stride, lane);
+    }
+    // the bias area: slot s of layer l's block is unit net_bias_unit(s)
+    const int s = (r0 * 64 + lane) * 4;                     // one float4 per lane
+    for (int s4 = s; s4 < a.g.bias_total; s4 += stride * 256) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) av[u][q] = 0.0f;
-            if (r >= rows) continue;
-            int64_t pb[4] = {-1, -1, -1, -1};               // flat index of each column
-            if (r < rows_w) {
-                int l = 0;
-                while (l + 1 < nl && r >= a.g.row0[l + 1]) ++l;
-                const int q = r - a.g.row0[l];
-                const int k = net_row_unit(l, q);
-                const int v = 4 * lane;
-                if (k < a.g.din[l] && v < a.g.dout[l]) {
-                    const int64_t p0 = a.g.flat_w[l] + static_cast<int64_t>(k) * a.g.dout[l] + v;
-                    dst[u] = img + a.g.img_off[l] + static_cast<int64_t>(q) * a.g.op[l] + v;
+        for (int l = 0; l < kNetL; ++l) {
+            if (l >= a.g.nl) break;
+            const int rel = s4 - a.g.bias_rel[l];
+            if (rel < 0 || rel >= a.g.op[l]) continue;
+            float *dst = img + a.g.bias_base + s4;
+            net_f4 w = *reinterpret_cast<const net_f4 *>(dst);
+            const float *b = act + a.g.flat_w[l] + static_cast<int64_t>(a.g.din[l]) * a.g.dout[l];
 #pragma unroll
-                    for (int c = 0; c < 4; ++c)
-                        if (v + c < a.g.dout[l]) pb[c] = p0 + c;
-                }
-            } else {
-                const int s = (r - rows_w) * 256 + 4 * lane;   // bias-area slot
-                if (s < a.g.bias_total) {
-                    int l = 0;
-                    while (l + 1 < nl && s >= a.g.bias_rel[l + 1]) ++l;
-                    dst[u] = img + a.g.bias_base + s;
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        const int un = net_bias_unit(s + c - a.g.bias_rel[l]);
-                        if (un < a.g.dout[l])
-                            pb[c] = a.g.flat_w[l] + static_cast<int64_t>(a.g.din[l]) * a.g.dout[l] + un;
-                    }
-                }
+            for (int c = 0; c < 4; ++c) {
+                const int un = net_bias_unit(rel + c);
+                if (un < a.g.dout[l]) w[c] -= b[un];
             }
-            if (!dst[u]) continue;
-            w[u] = *reinterpret_cast<const net_f4 *>(dst[u]);
-            if (pb[3] == pb[0] + 3 && ((reinterpret_cast<uintptr_t>(act + pb[0]) & 7) == 0)) {
-                const float2 lo = *reinterpret_cast<const float2 *>(act + pb[0]);
-                const float2 hi = *reinterpret_cast<const float2 *>(act + pb[0] + 2);
-                av[u][0] = lo.x;
-                av[u][1] = lo.y;
-                av[u][2] = hi.x;
-                av[u][3] = hi.y;
-            } else {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) av[u][c] = pb[c] >= 0 ? act[pb[c]] : 0.0f;
-            }
+            *reinterpret_cast<net_f4 *>(dst) = w;
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (dst[u])
-                *reinterpret_cast<net_f4 *>(dst[u]) =
-                    net_f4{w[u][0] - av[u][0], w[u][1] - av[u][1], w[u][2] - av[u][2], w[u][3] - av[u][3]};
     }
 }
 
@@ -199,52 +195,53 @@ __device__ __forceinline__ void net_half_mm(const float *sl, int s, int g, int n
     }
 }
 
-// Per-workgroup state of the forward's weight stream.  The two slots are
-// DISTINCT __shared__ arrays and every access names one statically: the
-// compiler then knows an LDS-DMA in flight into one slot does not alias the
-// reads of the other, and inserts no vmcnt wait before them (with a runtime
-// slot index it waited for the DMA before every read).
+// Per-workgroup state of the forward's weight stream.  The image's chunks
+// are contiguous in stream order (layer after layer; a layer-0 padding
+// chunk is not in the image), so the next chunk's source is a running
+// pointer and its width is known statically: no geometry lookup (a runtime
+// index into the kernel-argument arrays costs a memory round trip).  The two
+// slots are DISTINCT __shared__ arrays and every access names one
+// statically: the compiler then knows an LDS-DMA in flight into one slot
+// does not alias the reads of the other, and inserts no vmcnt wait before
+// them (with a runtime slot index it waited for the DMA before every read).
 struct NetStream {
-    const NetGeom *geo;
-    const float *img;
-    int wave, lane, total;
+    const float *next;               // source of the next chunk to load
+    int wave, lane;
 };
 
-// LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction) of chunk ci
-// into dst; a layer-0 padding chunk (layer 0 is padded to an even chunk
-// count, net_geometry) loads nothing
-__device__ __forceinline__ void net_issue(const NetStream &ws, int ci, float *dst) {
-    if (ci >= ws.total) return;
-    const NetGeom &g = *ws.geo;
-    int l = 0;
-    while (l + 1 < g.nl && ci >= g.chunk0[l + 1]) ++l;
-    const int lc = ci - g.chunk0[l];
-    if (lc >= g.nchunk[l]) return;
-    const int op = g.op[l];
-    const float *src = ws.img + g.img_off[l] + static_cast<int64_t>(lc) * kNetChunk * op;
+// LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction) of the next
+// chunk (32 rows x op floats) into dst; op == 0: nothing to load
+__device__ __forceinline__ void net_issue(NetStream &ws, int op, float *dst) {
+    if (op == 0) return;
     const int ninst = op >> 3;
     for (int k = ws.wave; k < ninst; k += kNetFwdWaves)
         __builtin_amdgcn_global_load_lds(
-            (__attribute__((address_space(1))) void *)(src + k * 256 + ws.lane * 4),
+            (__attribute__((address_space(1))) void *)(ws.next + k * 256 + ws.lane * 4),
             (__attribute__((address_space(3))) void *)(dst + k * 256), 16, 0, 0);
+    ws.next += kNetChunk * op;
 }
 
-// top of chunk ci: this wave's DMA (and X loads) of chunk ci landed, then the
-// workgroup's; the other slot is free for chunk ci + 1 (net_issue)
-// (the builtin, not inline asm: the compiler's wait tracking sees it and
+// top of a chunk: this wave's DMA (and X loads) of the chunk landed, then
+// the workgroup's; the other slot is free for the next chunk (net_issue).
+// (The builtin, not inline asm: the compiler's wait tracking sees it and
 // knows the X operands loaded with the chunk are in, instead of waiting for
-// them again behind the next DMA -- vmcnt counts in order)
+// them again behind the next DMA -- vmcnt counts in order.)
 __device__ __forceinline__ void net_chunk_wait() {
     __builtin_amdgcn_s_waitcnt(0x0f70);                     // vmcnt(0), expcnt / lgkmcnt untouched
     __syncthreads();
 }
 
-// Layer 0 over its chunks (padded to even): B operands from the Xt image,
-// prefetched a chunk ahead; slot A for even chunks, B for odd.
+// Layer 0 over its nch chunks, padded to even (slot A for even positions, B
+// for odd): B operands from the Xt image, prefetched a chunk ahead.
+// op_next: width of the next layer's chunks (loaded once this layer's are).
 template <int NCG>
-__device__ __forceinline__ void net_layer0(const NetStream &ws, int &ci, int nch, int F16,
+__device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, int F16,
                                            const float *xt, int g, int n, float *sa, float *sb,
                                            net_f4 (&hout)[16]) {
+    constexpr int op = 64 * NCG;
+    // what position q of the padded sequence loads: a real chunk, the padding
+    // (nothing), or the next layer's first chunk
+    auto op_at = [&](int q) { return q < nch ? op : (q == nch && (nch & 1) ? 0 : op_next); };
     net_f4 xn[2];
     auto xload = [&](int lc) {
 #pragma unroll
@@ -253,19 +250,19 @@ __device__ __forceinline__ void net_layer0(const NetStream &ws, int &ci, int nch
                                      : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
     };
     xload(0);
-    // the X operands are copied out before the next DMA issues: vmcnt counts
-    // in order, so a later use would wait for that DMA as well
-    for (int lc = 0; lc < nch; lc += 2, ci += 2) {
+    // the X operands are copied out before the next DMA issues (vmcnt counts
+    // in order: a later use would wait for that DMA as well)
+    for (int lc = 0; lc < nch; lc += 2) {
         net_chunk_wait();
         net_f4 x0 = xn[0], x1 = xn[1];
-        net_issue(ws, ci + 1, sb);
+        net_issue(ws, op_at(lc + 1), sb);
         if (lc + 1 < nch) xload(lc + 1);
         net_half_mm<NCG, true>(sa, 0, g, n, x0, hout);
         net_half_mm<NCG, true>(sa, 1, g, n, x1, hout);
         net_chunk_wait();
         x0 = xn[0];
         x1 = xn[1];
-        net_issue(ws, ci + 2, sa);
+        net_issue(ws, op_at(lc + 2), sa);
         if (lc + 1 < nch) {                                 // not the padding chunk
             if (lc + 2 < nch) xload(lc + 2);
             net_half_mm<NCG, true>(sb, 0, g, n, x0, hout);
@@ -278,17 +275,18 @@ __device__ __forceinline__ void net_layer0(const NetStream &ws, int &ci, int nch
 // units of input blocks (lc >> 1, 2 (lc & 1) + {0, 1}), B operands straight
 // from the previous layer's accumulators.  hin rotates down by four blocks
 // per chunk pair, so the loop keeps static register indices (fully unrolled
-// it spilled 4-28k VGPRs).
+// it spilled 4-28k VGPRs).  op_next: 0 after the output layer.
 template <int NCG>
-__device__ __forceinline__ void net_layer(const NetStream &ws, int &ci, int nch, int g, int n,
+__device__ __forceinline__ void net_layer(NetStream &ws, int nch, int op_next, int g, int n,
                                           float *sa, float *sb, net_f4 (&hin)[16], net_f4 (&hout)[16]) {
-    for (int lc = 0; lc < nch; lc += 2, ci += 2) {
+    constexpr int op = 64 * NCG;
+    for (int lc = 0; lc < nch; lc += 2) {
         net_chunk_wait();
-        net_issue(ws, ci + 1, sb);
+        net_issue(ws, op, sb);                              // lc + 1 < nch: nch is even
         net_half_mm<NCG, false>(sa, 0, g, n, hin[0], hout);
         net_half_mm<NCG, false>(sa, 1, g, n, hin[1], hout);
         net_chunk_wait();
-        net_issue(ws, ci + 2, sa);
+        net_issue(ws, lc + 2 < nch ? op : op_next, sa);
         net_half_mm<NCG, false>(sb, 0, g, n, hin[2], hout);
         net_half_mm<NCG, false>(sb, 1, g, n, hin[3], hout);
 #pragma unroll
@@ -297,9 +295,13 @@ __device__ __forceinline__ void net_layer(const NetStream &ws, int &ci, int nch,
 }
 
 // NCGH: 64-unit output groups of every hidden layer (net_geometry pads all
-// hidden widths to one op: 64 or 256); the output layer has one (K <= 32).
+// hidden widths to one op = 64 NCGH, 64 or 256); the output layer has one
+// (K <= 32).  So layer l's op, chunk count and bias offset are static
+// functions of l: op = 64 NCGH (hidden) / 64 (output), nchunk = 2 NCGH
+// (l >= 1), bias at l * 64 NCGH.
 template <int NCGH>
 __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
+    constexpr int OPH = 64 * NCGH;
     __shared__ __attribute__((aligned(16))) float slot_a[kNetSlotFloats];
     __shared__ __attribute__((aligned(16))) float slot_b[kNetSlotFloats];
     __shared__ __attribute__((aligned(16))) float sbias[kNetMaxBias];
@@ -319,7 +321,7 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     const bool rvalid = row < a.N;
     const float *img = a.img + static_cast<size_t>(e) * a.g.Pimg;
     const int nl = a.g.nl;
-    NetStream ws{&a.g, img, wave, lane, a.g.chunk0[nl]};
+    NetStream ws{img, wave, lane};
 
     for (int i = tid; i < a.g.bias_total; i += kNetThreads) sbias[i] = img[a.g.bias_base + i];
     int slot_n = -1;
@@ -330,25 +332,24 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     }
 
     net_f4 hin[16], hout[16];
-    auto bias_init = [&](int l) {
-        const int ncg = a.g.op[l] >> 6;
+    auto bias_init = [&](int l, int ncg) {
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 hout[c * 4 + j] = c < ncg ? *reinterpret_cast<const net_f4 *>(
-                                                &sbias[a.g.bias_rel[l] + ((c * 4 + j) * 4 + g) * 4])
+                                                &sbias[l * OPH + ((c * 4 + j) * 4 + g) * 4])
                                           : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
     };
+    auto op_of = [&](int l) { return l >= nl ? 0 : (l == nl - 1 ? 64 : OPH); };
 
-    net_issue(ws, 0, slot_a);
+    net_issue(ws, OPH, slot_a);
     __syncthreads();                                        // sbias
-    bias_init(0);
-    int ci = 0;
+    bias_init(0, NCGH);
 
     // ---- layer 0: K = the input features, B operand = X rows
     // (this wave's 16-row block of Xt, the lane's float4 of feature group 0)
-    net_layer0<NCGH>(ws, ci, a.g.nchunk[0], a.F16,
+    net_layer0<NCGH>(ws, a.g.nchunk[0], op_of(1), a.F16,
                      a.Xt + (static_cast<size_t>(tile * (kNetTile / 16) + wave) * a.F16 * 64 + lane) * 4,
                      g, n, slot_a, slot_b, hout);
 
@@ -356,7 +357,6 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     for (int l = 0; l + 1 < nl; ++l) {
         // hidden layer l done: relu (optimize_nn.py: Dense(relu)), the
         // minibatch rows' activations out, next layer's bias in the accumulators
-        const int op = a.g.op[l];
 #pragma unroll
         for (int c = 0; c < NCGH; ++c)
 #pragma unroll
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) hin[c * 4 + j][i] = fmaxf(hout[c * 4 + j][i], 0.0f);
         if (slot_n >= 0) {
-            float *dst = a.act_mb[l] + (static_cast<size_t>(e) * a.B + slot_n) * op;
+            float *dst = a.act_mb[l] + (static_cast<size_t>(e) * a.B + slot_n) * OPH;
 #pragma unroll
             for (int c = 0; c < NCGH; ++c)
 #pragma unroll
@@ -372,10 +372,13 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
                     *reinterpret_cast<net_f4 *>(dst + 64 * c + 16 * g + 4 * i) =
                         net_f4{hin[c * 4 + 0][i], hin[c * 4 + 1][i], hin[c * 4 + 2][i], hin[c * 4 + 3][i]};
         }
-        bias_init(l + 1);
-        if (l + 2 < nl) net_layer<NCGH>(ws, ci, a.g.nchunk[l + 1], g, n, slot_a, slot_b, hin, hout);
+        if (l + 2 < nl) {
+            bias_init(l + 1, NCGH);
+            net_layer<NCGH>(ws, 2 * NCGH, op_of(l + 2), g, n, slot_a, slot_b, hin, hout);
+        }
     }
-    net_layer<1>(ws, ci, a.g.nchunk[nl - 1], g, n, slot_a, slot_b, hin, hout);   // the output layer
+    bias_init(nl - 1, 1);
+    net_layer<1>(ws, 2 * NCGH, 0, g, n, slot_a, slot_b, hin, hout);   // the output layer
 
     // ---- logits -> softmax (utils_math.py:51-63), -log(p_y + 1e-16)
     // (utils_math.py:25-34), np.argmax's first maximum of P; class 16g + 4i + j
@@ -419,7 +422,7 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
         loss_r = static_cast<double>(-logf(py + 1e-16f));
         hit_r = arg == yl ? 1 : 0;
         if (slot_n >= 0) {
-            float *dz = a.dz_out + (static_cast<size_t>(e) * a.B + slot_n) * a.g.op[nl - 1];
+            float *dz = a.dz_out + (static_cast<size_t>(e) * a.B + slot_n) * 64;   // output op = 64
 #pragma unroll
             for (int k = 0; k < kNetMaxClasses; ++k)
                 if (k < K) dz[k] = z[k] - (k == yl ? 1.0f : 0.0f);
@@ -559,7 +562,12 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
         const int u0 = ut * 256 + 64 * wave;
         if (u0 >= dout) continue;                           // wave-uniform; no barriers here
         const int k0 = kt * 32, k = k0 + m;
-        // A: [H_{l-1} | 1] rows (layer 0: the dataset rows of sequence[0])
+        // A: [H_{l-1} | 1] rows (layer 0: the dataset rows of sequence[0]).
+        // Branch-free: clamped indices, every load of a batch issued before
+        // any is used, invalid entries zeroed by selects afterwards (a
+        // guarded load per step made two dependent round trips per step)
+        const bool kin = k < din, kone = k == din;
+        const int kc = kin ? k : din - 1;
         const float *Hin = nullptr;
         int hstride = 0;
         if (l > 0) {
@@ -571,32 +579,34 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
         net_f16 acc0 = {}, acc1 = {};
         const int steps = (a.B + 1) >> 1;
         for (int s0 = 0; s0 < steps; s0 += kNetGradBatch) {
+            int rr[kNetGradBatch];
             float xa[kNetGradBatch], b0[kNetGradBatch], b1[kNetGradBatch];
 #pragma unroll
             for (int q = 0; q < kNetGradBatch; ++q) {
                 const int r = 2 * (s0 + q) + h;
-                xa[q] = 0.0f;
-                b0[q] = 0.0f;
-                b1[q] = 0.0f;
-                if (r < a.B) {
-                    if (k < din) {
-                        if (l == 0) {
-                            const int xr = rows ? rows[r] : r;
-                            xa[q] = a.X[static_cast<size_t>(xr) * a.F + k];
-                        } else {
-                            xa[q] = Hin[static_cast<size_t>(r) * hstride + k];
-                        }
-                    } else if (k == din) {
-                        xa[q] = 1.0f;                       // the bias row
-                    }
-                    b0[q] = dz[static_cast<size_t>(r) * opl];
-                    b1[q] = dz[static_cast<size_t>(r) * opl + 32];
-                }
+                rr[q] = r < a.B ? r : a.B - 1;
+            }
+            if (l == 0) {                                   // wave-uniform
+                int xr[kNetGradBatch];
+#pragma unroll
+                for (int q = 0; q < kNetGradBatch; ++q) xr[q] = rows ? rows[rr[q]] : rr[q];
+#pragma unroll
+                for (int q = 0; q < kNetGradBatch; ++q) xa[q] = a.X[static_cast<size_t>(xr[q]) * a.F + kc];
+            } else {
+#pragma unroll
+                for (int q = 0; q < kNetGradBatch; ++q) xa[q] = Hin[static_cast<size_t>(rr[q]) * hstride + kc];
             }
 #pragma unroll
             for (int q = 0; q < kNetGradBatch; ++q) {
-                acc0 = net_mfma32(xa[q], b0[q], acc0);
-                acc1 = net_mfma32(xa[q], b1[q], acc1);
+                b0[q] = dz[static_cast<size_t>(rr[q]) * opl];
+                b1[q] = dz[static_cast<size_t>(rr[q]) * opl + 32];
+            }
+#pragma unroll
+            for (int q = 0; q < kNetGradBatch; ++q) {
+                const bool ok = 2 * (s0 + q) + h < a.B;
+                const float av = ok ? (kin ? xa[q] : (kone ? 1.0f : 0.0f)) : 0.0f;   // the bias row: 1
+                acc0 = net_mfma32(av, ok ? b0[q] : 0.0f, acc0);
+                acc1 = net_mfma32(av, ok ? b1[q] : 0.0f, acc1);
             }
         }
         // epilogue: accumulator r of lane (h, m) = row k0 + 8(r>>2) + 4h + (r&3)
@@ -608,10 +618,11 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
             const int u = u0 + 32 * bb + m;
             const net_f16 &acc = bb ? acc1 : acc0;
             double gold[16];
+            const int uc = u < dout ? u : dout - 1;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+            for (int r = 0; r < 16; ++r) {                  // clamped: every load unconditional
                 const int kk = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
-                gold[r] = (kk <= din && u < dout) ? G[fw + static_cast<int64_t>(kk) * dout + u] : 0.0;
+                gold[r] = G[fw + static_cast<int64_t>(kk <= din ? kk : din) * dout + uc];
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
