@@ -68,6 +68,13 @@ typedef double lr_d4 __attribute__((ext_vector_type(4)));
 #ifndef CE_LR_WT
 #define CE_LR_WT 1
 #endif
+//  CE_LR_OBS_STAGE the workgroup's observation block (16 envs x obs_stride
+//                 floats: line-aligned, whole lines) is assembled in LDS and
+//                 stored 16 B per lane in line order, instead of the zero,
+//                 L' and G' pieces each storing a part of every line
+#ifndef CE_LR_OBS_STAGE
+#define CE_LR_OBS_STAGE 0
+#endif
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
 
@@ -211,6 +218,9 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     __shared__ double red_l[kLrWaves][kLrEnvs];         // per-wave -log CE partials
     __shared__ double red_h[kLrWaves][kLrEnvs];         // per-wave hit counts
     __shared__ __attribute__((aligned(16))) double wsh[kLrEnvs][P_MAX];   // W' of the group's envs
+#if CE_LR_OBS_STAGE
+    __shared__ __attribute__((aligned(16))) float obs_s[kLrEnvs * (2 * P_MAX + 4)];
+#endif
 #ifdef CE_DIAG
     unsigned long long stamps[kStamps] = {0};
     stamps[6] = __builtin_amdgcn_s_memrealtime();
@@ -528,9 +538,15 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     // has consumed its loads (vmcnt counts stores as well): the
     // observation's weight part (wght_hist is identically 0), done and the
     // episode length
+#if CE_LR_OBS_STAGE
+#pragma unroll
+    for (int r = 0; r < PR; ++r)
+        if (prole[r] && OL == 0) obs_s[pj[r] * OS + pp[r]] = 0.0f;
+#else
 #pragma unroll
     for (int r = 0; r < PR; ++r)
         if (prole[r] && OL == 0) lr_store(&a.obs[static_cast<unsigned>(e0 + pj[r]) * OS + pp[r]], 0.0f);
+#endif
     if (srole) {
         if (a.done) a.done[es] = cur >= a.max_steps ? 1 : 0;
         lr_store(&a.episode_len[es], cur);
@@ -575,7 +591,11 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
         if (a.reward) lr_store(&a.reward[es], static_cast<float>(-loss));   // compact: -objective
         lr_store(&a.objective[es], static_cast<float>(loss));   // B == N: the same numbers
         lr_store(&a.accuracy[es], static_cast<float>(acc));
+#if CE_LR_OBS_STAGE
+        obs_s[sj * OS + P - OL] = wipe ? 0.0f : static_cast<float>(lnew);
+#else
         lr_store(&a.obs[es * OS + P - OL], wipe ? 0.0f : static_cast<float>(lnew));
+#endif
         lr_store(&Lp[es], wipe ? 0.0 : lnew);
         lr_store(&stepp[es], wipe ? 0 : cur);
     }
@@ -591,11 +611,29 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
         for (int w = 0; w < kLrWaves; ++w) sf += red_s[w][f >> 2][pj[r] + 16 * (f & 3)];
         const double g = div_rcp((pp[r] & 1) ? sf : -sf, dB, rB);
         const double gnew = div_rcp(g, fabs(g_prev[r]) + 1.0, rG[r]);
+#if CE_LR_OBS_STAGE
+        obs_s[pj[r] * OS + P + 1 + pp[r] - OL] = wipe ? 0.0f : static_cast<float>(gnew);
+#else
         lr_store(&a.obs[static_cast<unsigned>(e0 + pj[r]) * OS + P + 1 + pp[r] - OL],
                  wipe ? 0.0f : static_cast<float>(gnew));
+#endif
         lr_store(&Wp[gi[r]], wipe ? w_init[r] : wsh[pj[r]][pp[r]]);
         lr_store(&Gp[gi[r]], wipe ? 0.0 : gnew);
     }
+#if CE_LR_OBS_STAGE
+    __syncthreads();
+    {   // the block [e0 OS, (e0 + nenv) OS) floats: 64-B aligned (16 OS floats per full group)
+        const int nenv = Ep - e0 < kLrEnvs ? Ep - e0 : kLrEnvs;
+        const int nfl = nenv * OS, n4 = nfl >> 2;
+        float *ob = a.obs + static_cast<unsigned>(e0) * OS;
+        for (int i = tid; i < n4; i += kLrBlock) {
+            typedef float lr_f4 __attribute__((ext_vector_type(4)));
+            const lr_f4 v = *reinterpret_cast<const lr_f4 *>(&obs_s[4 * i]);
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(ob + 4 * i), "v"(v) : "memory");
+        }
+        for (int i = 4 * n4 + tid; i < nfl; i += kLrBlock) lr_store(&ob[i], obs_s[i]);
+    }
+#endif
     CE_STAMP(4);
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -75,7 +75,11 @@ def summarize(src_fetch, src_write, step_kernel, envs, name, rnd, bpe=None, extr
         out['traffic_over_algorithmic'] = (total_r + total_w) / (bpe * envs)
     if extra:
         out.update(extra)
-    path = os.path.join(ROOT, 'profiles', '%s_traffic_%s.json' % (rnd, name))
+    # CE_TRAFFIC_OUT: where to write (a GPU box returns only gpurun_out/;
+    # the committed copies live in profiles/)
+    out_dir = os.environ.get('CE_TRAFFIC_OUT', os.path.join(ROOT, 'profiles'))
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, '%s_traffic_%s.json' % (rnd, name))
     with open(path, 'w') as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     return out, path
@@ -85,11 +89,12 @@ def collect(rnd, name, bench_args, out_dir, limit=150):
     """Two counter passes of bench.py as child processes (never exec'd from a
     process that touched the GPU), each killed at `limit` seconds."""
     dirs = {}
+    os.makedirs(out_dir, exist_ok=True)
     for counter in ('FETCH_SIZE', 'WRITE_SIZE'):
         d = os.path.join(out_dir, counter.lower())
         cmd = ['timeout', '-s', 'KILL', str(limit), 'rocprofv3', '--pmc', counter, '-d', d, '-o', 'run',
                '--output-format', 'csv', '--', sys.executable, os.path.join(ROOT, 'bench.py')] + bench_args
-        with open(d + '.log', 'w') if os.path.isdir(os.path.dirname(d)) else open(os.devnull, 'w') as log:
+        with open(d + '.log', 'w') as log:
             rc = subprocess.call(cmd, cwd=ROOT, stdout=log, stderr=subprocess.STDOUT,
                                  env=dict(os.environ, TMPDIR=os.environ.get('TMPDIR', '/tmp')))
         if rc != 0:
