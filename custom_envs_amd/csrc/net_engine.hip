@@ -201,7 +201,7 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
     int task = 0;
     for (int l = 0; l < nl; ++l) {
         p->task0[l] = task;
-        p->ut[l] = (geo.dout[l] + 255) / 256;
+        p->ut[l] = (geo.dout[l] + kNetGradTile - 1) / kNetGradTile;
         task += (geo.din[l] + 1 + 31) / 32 * p->ut[l];
     }
     p->task0[nl] = task;

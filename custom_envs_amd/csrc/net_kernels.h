@@ -515,13 +515,13 @@ __global__ __launch_bounds__(kNetThreads) void net_bwd_kernel(NetBwdArgs a) {
 // numpy divides the float32 gradient), G' = g / (|G| + 1) in float64
 // (grad_hist float64, optimize.py:78-83), obs = [0 (P) | L' | G' (P)]; an env
 // whose step ends its episode (utils_venv.py:31) writes the reset
-// observation and G <- 0.  Workgroup = 32 rows of [dW; db] x 256 units of one
-// layer of one env; wave = 64 units (two 32x32 blocks).
+// observation and G <- 0.  Workgroup = 32 rows of [dW; db] x kNetGradTile units of one
+// layer of one env; wave = 32 kNetGradWaveBlocks units (32x32 blocks).
 struct NetGradArgs {
     NetGeom g;
     int E, N, B, P, F, max_steps, auto_reset, tpe;
     int task0[kNetL + 1];            // first task of layer l within an env
-    int ut[kNetL];                   // 256-unit tiles of layer l
+    int ut[kNetL];                   // kNetGradTile-unit tiles of layer l
     const float *X;                  // [N][F]
     const int32_t *order;            // [2][E][N] (nullptr: B == N, rows in order)
     const int32_t *order_sel;
@@ -540,6 +540,14 @@ __device__ __forceinline__ net_f16 net_mfma32(float a, float b, net_f16 c) {
 // K steps of the [dW; db] product loaded in one batch (their loads in flight
 // together, then the MFMAs)
 constexpr int kNetGradBatch = 16;
+// 32-unit accumulator blocks per wave (CE_NET_GRAD_BLOCKS, build-time A/B):
+// 2 = a 256-unit workgroup tile, 1 = 128 units and half the accumulator and
+// float64 epilogue registers (more waves in flight on the gathers)
+#ifndef CE_NET_GRAD_BLOCKS
+#define CE_NET_GRAD_BLOCKS 2
+#endif
+constexpr int kNetGradWaveBlocks = CE_NET_GRAD_BLOCKS;
+constexpr int kNetGradTile = 4 * 32 * kNetGradWaveBlocks;   // units per workgroup task
 
 __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
     const int e = blockIdx.y;
@@ -559,7 +567,7 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
         const int tl = task - a.task0[l];
         const int kt = tl / a.ut[l], ut = tl - kt * a.ut[l];
         const int din = a.g.din[l], dout = a.g.dout[l];
-        const int u0 = ut * 256 + 64 * wave;
+        const int u0 = ut * kNetGradTile + 32 * kNetGradWaveBlocks * wave;
         if (u0 >= dout) continue;                           // wave-uniform; no barriers here
         const int k0 = kt * 32, k = k0 + m;
         // A: [H_{l-1} | 1] rows (layer 0: the dataset rows of sequence[0]).
@@ -576,11 +584,11 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
         }
         const int opl = a.g.op[l];
         const float *dz = (l + 1 == nl ? a.dz_out : a.dz_mb[l]) + static_cast<size_t>(e) * a.B * opl + u0 + m;
-        net_f16 acc0 = {}, acc1 = {};
+        net_f16 acc[kNetGradWaveBlocks] = {};
         const int steps = (a.B + 1) >> 1;
         for (int s0 = 0; s0 < steps; s0 += kNetGradBatch) {
             int rr[kNetGradBatch];
-            float xa[kNetGradBatch], b0[kNetGradBatch], b1[kNetGradBatch];
+            float xa[kNetGradBatch], bz[kNetGradWaveBlocks][kNetGradBatch];
 #pragma unroll
             for (int q = 0; q < kNetGradBatch; ++q) {
                 const int r = 2 * (s0 + q) + h;
@@ -597,16 +605,17 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
                 for (int q = 0; q < kNetGradBatch; ++q) xa[q] = Hin[static_cast<size_t>(rr[q]) * hstride + kc];
             }
 #pragma unroll
-            for (int q = 0; q < kNetGradBatch; ++q) {
-                b0[q] = dz[static_cast<size_t>(rr[q]) * opl];
-                b1[q] = dz[static_cast<size_t>(rr[q]) * opl + 32];
-            }
+            for (int q = 0; q < kNetGradBatch; ++q)
+#pragma unroll
+                for (int bb = 0; bb < kNetGradWaveBlocks; ++bb)
+                    bz[bb][q] = dz[static_cast<size_t>(rr[q]) * opl + 32 * bb];
 #pragma unroll
             for (int q = 0; q < kNetGradBatch; ++q) {
                 const bool ok = 2 * (s0 + q) + h < a.B;
                 const float av = ok ? (kin ? xa[q] : (kone ? 1.0f : 0.0f)) : 0.0f;   // the bias row: 1
-                acc0 = net_mfma32(av, ok ? b0[q] : 0.0f, acc0);
-                acc1 = net_mfma32(av, ok ? b1[q] : 0.0f, acc1);
+#pragma unroll
+                for (int bb = 0; bb < kNetGradWaveBlocks; ++bb)
+                    acc[bb] = net_mfma32(av, ok ? bz[bb][q] : 0.0f, acc[bb]);
             }
         }
         // epilogue: accumulator r of lane (h, m) = row k0 + 8(r>>2) + 4h + (r&3)
@@ -614,9 +623,8 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
         // before its stores
         const int64_t fw = a.g.flat_w[l];
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
+        for (int bb = 0; bb < kNetGradWaveBlocks; ++bb) {
             const int u = u0 + 32 * bb + m;
-            const net_f16 &acc = bb ? acc1 : acc0;
             double gold[16];
             const int uc = u < dout ? u : dout - 1;
 #pragma unroll
@@ -629,7 +637,7 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
                 const int kk = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
                 if (kk > din || u >= dout) continue;
                 const int64_t p = fw + static_cast<int64_t>(kk) * dout + u;
-                const float gv = acc[r] / fB;
+                const float gv = acc[bb][r] / fB;
                 const double gn = static_cast<double>(gv) / (fabs(gold[r]) + 1.0);
                 obs[p] = 0.0f;                              // wght_hist is identically 0
                 obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(gn);

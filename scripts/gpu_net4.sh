@@ -16,5 +16,9 @@ tail -1 $OUT/bench_net.log | cut -c1-400; fatal $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_net -o run --output-format csv -- python3 bench.py --workload mlp --hidden 256,256 --batch-size 32 --envs 1024 --profile-only --steps 5 --warmup 1 > $OUT/prof_net.log 2>&1; rc=$?
 echo "prof rc=$rc"; fatal $rc
 find $OUT/prof_net -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-200 | head -20
+for V in ${NETVARIANTS:-}; do
+  CE_LIB=$V timeout -k 10 300 python bench.py --workload mlp --hidden 256,256 --batch-size 32 --envs 1024 --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_net_$V.log 2>&1; rc=$?
+  echo "variant $V: $(tail -1 $OUT/bench_net_$V.log | cut -c1-160)"; fatal $rc
+done
 [ -n "${PMC:-}" ] && { OUT=$OUT/pmc bash scripts/gpu_pmc_net.sh || exit $?; }
 echo ALL_OK
