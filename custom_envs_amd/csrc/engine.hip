@@ -987,10 +987,6 @@ int ce_set_state(ce_engine *e, const ce_state *st) {
         if (!e->order) return fail(CE_ESTATE, "row order is only tracked when batch_size < n_rows");
         CE_HIP(hipMemcpy(e->order, st->order, E * N * sizeof(int32_t), hipMemcpyHostToDevice));
         CE_HIP(hipMemset(e->order_sel, 0, E * sizeof(int32_t)));
-        if (e->net) {   // the minibatch slots of the new order
-            const ce::NetArgs a = make_net_args(e, nullptr, region_view(e, e->d_out));
-            if ((rc = ce::net_sync_order(e->net, a, e->stream)) != CE_OK) return rc;
-        }
     }
     CE_HIP(hipStreamSynchronize(e->stream));
     e->was_reset = true;

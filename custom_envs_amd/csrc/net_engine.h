@@ -99,16 +99,16 @@ struct NetArgs {
 struct NetPlan;
 
 // Work buffers for E envs of this shape (the dataset in MFMA operand order,
-// the minibatch slots of every row, the minibatch activations and dZ).
+// the gathered minibatch rows, their activations and dZ) and the side stream
+// the gradient chain runs on.
 int net_create(NetPlan **out, const NetArgs &shape, int device);
 void net_destroy(NetPlan *plan);
 const NetGeom &net_geom(const NetPlan *plan);
 // Stream-ordered launches of one step / one reset (no host synchronisation:
-// capturable into a hipGraph).
+// capturable into a hipGraph -- the step forks onto the plan's side stream
+// and joins back with events, the capture pattern).
 int net_step(NetPlan *plan, const NetArgs &a, hipStream_t stream);
 int net_reset(NetPlan *plan, const NetArgs &a, hipStream_t stream);
-// after ce_set_state wrote a row order: the minibatch slots of that order
-int net_sync_order(NetPlan *plan, const NetArgs &a, hipStream_t stream);
 // Flat parameter count of the network.
 int64_t net_params(int F, int K, int n_hidden, const int *hidden);
 

@@ -112,10 +112,17 @@ void net_image_to_flat(const NetGeom &g, const float *img, float *flat) {
 struct NetPlan {
     NetGeom g;
     int E = 0, N = 0, B = 0, T = 0, F16 = 0;
+    int Tmb = 0;                             // minibatch tiles (B < N)
     float *Xt = nullptr;                     // [T*64/16][F16][64][4]
-    int32_t *mb_slot = nullptr;              // [E][N] (B < N)
-    double *part_loss = nullptr;             // [E][T][2]
+    float *Xmb = nullptr;                    // [E][Tmb*64/16][F16][64][4] (B < N)
+    int32_t *label_mb = nullptr;             // [E][Tmb*64] (B < N)
+    double *part_loss = nullptr;             // [E][T]: info forward
     int32_t *part_hits = nullptr;
+    double *mb_loss = nullptr;               // [E][Tmb]: minibatch forward (B < N)
+    int32_t *mb_hits = nullptr;
+    hipStream_t side = nullptr;              // the gradient chain
+    hipStream_t fwd = nullptr;               // the info forward
+    hipEvent_t fork = nullptr, join = nullptr, fwd_done = nullptr;
     float *act_mb[kNetL] = {nullptr};        // hidden l: [E][B][op_l]
     float *dz_mb[kNetL] = {nullptr};         // hidden l: [E][B][op_l]
     float *dz_out = nullptr;                 // [E][B][op_{nl-1}]
@@ -183,14 +190,30 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
         CE_HIP(hipMemcpy(p->Xt, xt.data(), xt.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     if (B < N) {
-        if ((rc = dev_alloc(&p->mb_slot, E * N)) != CE_OK) return bail(rc);
-        std::vector<int32_t> slots(E * N);
-        for (size_t e = 0; e < E; ++e)
-            for (size_t r = 0; r < N; ++r) slots[e * N + r] = r < B ? static_cast<int32_t>(r) : -1;
-        CE_HIP(hipMemcpy(p->mb_slot, slots.data(), slots.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        p->Tmb = (a.B + kNetTile - 1) / kNetTile;
+        const size_t rows = static_cast<size_t>(p->Tmb) * kNetTile;
+        if ((rc = dev_alloc(&p->Xmb, E * rows * p->F16 * 16, true)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->label_mb, E * rows, true)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->mb_loss, E * p->Tmb, true)) != CE_OK) return bail(rc);
+        if ((rc = dev_alloc(&p->mb_hits, E * p->Tmb, true)) != CE_OK) return bail(rc);
     }
-    if ((rc = dev_alloc(&p->part_loss, E * p->T * 2, true)) != CE_OK) return bail(rc);
-    if ((rc = dev_alloc(&p->part_hits, E * p->T * 2, true)) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->part_loss, E * p->T, true)) != CE_OK) return bail(rc);
+    if ((rc = dev_alloc(&p->part_hits, E * p->T, true)) != CE_OK) return bail(rc);
+    // CE_NET_SIDE_PRIO = 1: the info forward on a stream of the greatest
+    // priority, so a slot the forward frees goes to its next workgroup before
+    // the gradient chain's
+#ifndef CE_NET_SIDE_PRIO
+#define CE_NET_SIDE_PRIO 0
+#endif
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&p->fwd, hipStreamNonBlocking, CE_NET_SIDE_PRIO ? prio_hi : prio_lo) !=
+            hipSuccess ||
+        hipEventCreateWithFlags(&p->fwd_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&p->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&p->join, hipEventDisableTiming) != hipSuccess)
+        return bail(fail(CE_EHIP, "network: side stream / events"));
     const int nl = geo.nl;
     for (int l = 0; l + 1 < nl; ++l) {
         if ((rc = dev_alloc(&p->act_mb[l], E * B * geo.op[l], true)) != CE_OK) return bail(rc);
@@ -217,9 +240,14 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
 
 void net_destroy(NetPlan *p) {
     if (!p) return;
-    void *bufs[] = {p->Xt, p->mb_slot, p->part_loss, p->part_hits, p->dz_out};
+    void *bufs[] = {p->Xt, p->Xmb, p->label_mb, p->part_loss, p->part_hits, p->mb_loss, p->mb_hits, p->dz_out};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    if (p->fork) (void)hipEventDestroy(p->fork);
+    if (p->join) (void)hipEventDestroy(p->join);
+    if (p->fwd_done) (void)hipEventDestroy(p->fwd_done);
+    if (p->side) (void)hipStreamDestroy(p->side);
+    if (p->fwd) (void)hipStreamDestroy(p->fwd);
     for (int l = 0; l < kNetL; ++l) {
         if (p->act_mb[l]) (void)hipFree(p->act_mb[l]);
         if (p->dz_mb[l]) (void)hipFree(p->dz_mb[l]);
@@ -241,6 +269,10 @@ NetFinArgs fin_args(const NetPlan *p, const NetArgs &a) {
     f.Pimg = p->g.Pimg;
     f.part_loss = p->part_loss;
     f.part_hits = p->part_hits;
+    // B == N: the info forward is the minibatch forward
+    f.Tmb = p->Tmb ? p->Tmb : p->T;
+    f.mb_loss = p->Tmb ? p->mb_loss : p->part_loss;
+    f.mb_hits = p->Tmb ? p->mb_hits : p->part_hits;
     f.img = a.W;
     f.img0 = a.W0;
     f.L = a.L;
@@ -248,7 +280,6 @@ NetFinArgs fin_args(const NetPlan *p, const NetArgs &a) {
     f.perm = a.perm;
     f.order = a.order;
     f.order_sel = a.order_sel;
-    f.mb_slot = p->mb_slot;
     f.obs = a.obs;
     f.reward = a.reward;
     f.done = a.done;
@@ -273,27 +304,66 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         u.step = a.step;
         hipLaunchKernelGGL(net_update_kernel, dim3(p->upd_blocks, E), dim3(kNetThreads), 0, s, u);
     }
-    {
+    const bool split = p->Tmb > 0;                          // B < N: a separate minibatch forward
+    auto forward = [&](bool mb, hipStream_t st) {
         NetFwdArgs f{};
         f.g = g;
         f.E = E;
-        f.N = a.N;
-        f.B = a.B;
-        f.T = p->T;
         f.F16 = p->F16;
         f.img = a.W;
-        f.Xt = p->Xt;
-        f.label = a.label;
-        f.mb_slot = p->mb_slot;
-        f.part_loss = p->part_loss;
-        f.part_hits = p->part_hits;
+        if (mb && split) {
+            f.rows = a.B;
+            f.T = p->Tmb;
+            f.Xt = p->Xmb;
+            f.xt_env = static_cast<int64_t>(p->Tmb) * kNetTile * p->F16 * 16;
+            f.label = p->label_mb;
+            f.label_env = static_cast<int64_t>(p->Tmb) * kNetTile;
+            f.part_loss = p->mb_loss;
+            f.part_hits = p->mb_hits;
+        } else {
+            f.rows = a.N;
+            f.T = p->T;
+            f.Xt = p->Xt;
+            f.label = a.label;
+            f.part_loss = p->part_loss;
+            f.part_hits = p->part_hits;
+        }
+        f.mb = mb ? 1 : 0;
         for (int l = 0; l < kNetL; ++l) f.act_mb[l] = p->act_mb[l];
         f.dz_out = p->dz_out;
-        const unsigned grid = static_cast<unsigned>((E + 7) / 8 * 8) * p->T;
+        const unsigned grid = static_cast<unsigned>((E + 7) / 8 * 8) * f.T;
         if (g.op[0] == kNetMaxOp)
-            hipLaunchKernelGGL(net_fwd_kernel<kNetMaxOp / 64>, dim3(grid), dim3(kNetThreads), 0, s, f);
+            hipLaunchKernelGGL(net_fwd_kernel<kNetMaxOp / 64>, dim3(grid), dim3(kNetThreads), 0, st, f);
         else
-            hipLaunchKernelGGL(net_fwd_kernel<1>, dim3(grid), dim3(kNetThreads), 0, s, f);
+            hipLaunchKernelGGL(net_fwd_kernel<1>, dim3(grid), dim3(kNetThreads), 0, st, f);
+    };
+    if (split) {
+        NetGatherArgs ga{};
+        ga.E = E;
+        ga.N = a.N;
+        ga.B = a.B;
+        ga.F = a.F;
+        ga.F16 = p->F16;
+        ga.Tmb = p->Tmb;
+        ga.X = a.X;
+        ga.label = a.label;
+        ga.order = a.order;
+        ga.order_sel = a.order_sel;
+        ga.Xmb = p->Xmb;
+        ga.label_mb = p->label_mb;
+        hipLaunchKernelGGL(net_gather_kernel, dim3(p->Tmb * (kNetTile / 16), E), dim3(kNetThreads), 0, s, ga);
+    }
+    // the minibatch forward (B == N: the info forward too), then the fork:
+    // the info forward on this stream, the gradient chain on the side stream
+    forward(true, s);
+    hipStream_t gs = s;
+    if (split) {
+        CE_HIP(hipEventRecord(p->fork, s));
+        CE_HIP(hipStreamWaitEvent(p->fwd, p->fork, 0));
+        CE_HIP(hipStreamWaitEvent(p->side, p->fork, 0));
+        forward(false, p->fwd);                             // first: it takes its 2 workgroups per CU
+        CE_HIP(hipEventRecord(p->fwd_done, p->fwd));
+        gs = p->side;
     }
     for (int lh = nl - 2; lh >= 0; --lh) {
         NetBwdArgs b{};
@@ -305,7 +375,7 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         b.dz_next = lh + 1 == nl - 1 ? p->dz_out : p->dz_mb[lh + 1];
         b.act = p->act_mb[lh];
         b.dz = p->dz_mb[lh];
-        hipLaunchKernelGGL(net_bwd_kernel, dim3(E), dim3(kNetThreads), 0, s, b);
+        hipLaunchKernelGGL(net_bwd_kernel, dim3(E), dim3(kNetThreads), 0, gs, b);
     }
     {
         NetGradArgs r{};
@@ -332,7 +402,12 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         r.G = a.G;
         r.obs = a.obs;
         hipLaunchKernelGGL(net_grad_kernel, dim3(std::min(p->tpe, kNetGradBlocks), E), dim3(kNetThreads),
-                           0, s, r);
+                           0, gs, r);
+    }
+    if (split) {
+        CE_HIP(hipEventRecord(p->join, p->side));
+        CE_HIP(hipStreamWaitEvent(s, p->fwd_done, 0));
+        CE_HIP(hipStreamWaitEvent(s, p->join, 0));
     }
     hipLaunchKernelGGL(net_finish_kernel, dim3(E), dim3(kNetThreads), 0, s, fin_args(p, a));
     CE_HIP(hipGetLastError());
@@ -356,11 +431,5 @@ int net_reset(NetPlan *p, const NetArgs &a, hipStream_t s) {
     return CE_OK;
 }
 
-int net_sync_order(NetPlan *p, const NetArgs &a, hipStream_t s) {
-    if (!p->mb_slot || !a.order) return CE_OK;
-    hipLaunchKernelGGL(net_slots_kernel, dim3(a.E), dim3(kNetThreads), 0, s, fin_args(p, a));
-    CE_HIP(hipGetLastError());
-    return CE_OK;
-}
 
 }  // namespace ce

@@ -4,22 +4,27 @@
 // No library GEMM: every dense product runs on v_mfma_f32_16x16x4_f32 /
 // v_mfma_f32_32x32x2_f32 issued from these kernels.
 //
-// One VecEnv.step is five stream-ordered launches (net_engine.hip):
+// One VecEnv.step (net_engine.hip), two streams:
 //   net_update_kernel  W' = W - a into the env's weight IMAGE (below), step += 1
-//   net_fwd_kernel     the forward of every dataset row (info['objective'] /
-//                      ['accuracy'], optimize.py:94-97) -- 64 rows x one env per
-//                      workgroup, the whole layer chain in registers; the rows
-//                      of the env's minibatch (sequence[0]) also leave their
-//                      activations and dZ = P - Y, and their loss / hits: the
-//                      minibatch forward is a subset of the full-data forward
-//                      under the same W' (optimize.py:74-76 then :94-96)
-//   net_bwd_kernel     dZ_l = (dZ_{l+1} W_{l+1}^T) * relu'(H_l), one hidden
-//                      layer per launch, top down
-//   net_grad_kernel    [dW_l; db_l] = [H_{l-1} | 1]^T dZ_l on MFMA, and in the
-//                      same registers the float64 epilogue G' = (g / B) /
-//                      (|G| + 1), obs = [0 | L' | G'] (optimize.py:78-91)
+//   net_gather_kernel  the env's minibatch rows (sequence[0] of its row order)
+//                      into the forward's B-operand layout, with their labels
+//   net_fwd_kernel     (minibatch mode) the minibatch forward: activations,
+//                      dZ = P - Y, loss / hits (optimize.py:74-76)
+//   then, concurrently:
+//     main stream  net_fwd_kernel (info mode): the forward of every dataset
+//                  row (info['objective'] / ['accuracy'], optimize.py:94-97)
+//                  -- 64 rows x one env per workgroup, the whole layer chain
+//                  in registers; MFMA-bound
+//     side stream  net_bwd_kernel: dZ_l = (dZ_{l+1} W_{l+1}^T) * relu'(H_l),
+//                  one hidden layer per launch, top down; net_grad_kernel:
+//                  [dW_l; db_l] = [H_{l-1} | 1]^T dZ_l on MFMA, and in the same
+//                  registers the float64 epilogue G' = (g / B) / (|G| + 1),
+//                  obs = [0 | L' | G'] (optimize.py:78-91); HBM-bound, so it
+//                  runs in the VGPRs / issue slots the forward leaves free
 //   net_finish_kernel  per env: L', reward, done, info, the auto-reset
 //                      (utils_venv.py:31: W <- W0, order <- order[perm])
+// With B == N (full batch) the two forwards are one: the info forward also
+// leaves the minibatch outputs, and the chain after it is serial.
 //
 // The weight IMAGE of an env (floats, NetGeom::Pimg per env) is the layout the
 // forward streams through LDS by LDS-DMA (global_load_lds_dwordx4), one
@@ -148,15 +153,19 @@ __global__ __launch_bounds__(kNetThreads) void net_update_kernel(NetUpdArgs a) {
 // ci + 1 is loaded into registers while chunk ci is multiplied, and written
 // to the free slot after it (register staging: an LDS-DMA in flight makes
 // the compiler wait for it before every LDS read).
+// Two modes: info (rows = N, the shared dataset image, no stores but the
+// partials) and minibatch (mb = 1: rows = B, the env's gathered rows; row r is
+// minibatch slot r and leaves its activations and dZ).
 struct NetFwdArgs {
     NetGeom g;
-    int E, N, B, T, F16;
+    int E, rows, T, F16, mb;
     const float *img;                // [E][Pimg]
-    const float *Xt;                 // [Nt / 16][F16][64 lanes][4]: X in B-operand order
-    const int32_t *label;            // [N]
-    const int32_t *mb_slot;          // [E][N]: minibatch slot of a row or -1 (nullptr: B == N)
-    double *part_loss;               // [E][T][2]: info, minibatch
-    int32_t *part_hits;              // [E][T][2]
+    const float *Xt;                 // [T * 4][F16][64 lanes][4]: rows in B-operand order
+    int64_t xt_env;                  // floats between envs' Xt (0: shared)
+    const int32_t *label;            // [T * 64] per env
+    int64_t label_env;               // ints between envs' labels (0: shared)
+    double *part_loss;               // [E][T]
+    int32_t *part_hits;              // [E][T]
     float *act_mb[kNetL];            // hidden layer l: [E][B][op_l] post-relu minibatch rows
     float *dz_out;                   // [E][B][op_{nl-1}] P - Y of the minibatch rows
 };
@@ -237,7 +246,7 @@ __device__ __forceinline__ void net_chunk_wait() {
 template <int NCG>
 __device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, int F16,
                                            const float *xt, int g, int n, float *sa, float *sb,
-                                           net_f4 (&hout)[16]) {
+                                           bool active, net_f4 (&hout)[16]) {
     constexpr int op = 64 * NCG;
     // what position q of the padded sequence loads: a real chunk, the padding
     // (nothing), or the next layer's first chunk
@@ -257,13 +266,15 @@ __device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, 
         net_f4 x0 = xn[0], x1 = xn[1];
         net_issue(ws, op_at(lc + 1), sb);
         if (lc + 1 < nch) xload(lc + 1);
-        net_half_mm<NCG, true>(sa, 0, g, n, x0, hout);
-        net_half_mm<NCG, true>(sa, 1, g, n, x1, hout);
+        if (active) {
+            net_half_mm<NCG, true>(sa, 0, g, n, x0, hout);
+            net_half_mm<NCG, true>(sa, 1, g, n, x1, hout);
+        }
         net_chunk_wait();
         x0 = xn[0];
         x1 = xn[1];
         net_issue(ws, op_at(lc + 2), sa);
-        if (lc + 1 < nch) {                                 // not the padding chunk
+        if (lc + 1 < nch && active) {                       // not the padding chunk
             if (lc + 2 < nch) xload(lc + 2);
             net_half_mm<NCG, true>(sb, 0, g, n, x0, hout);
             net_half_mm<NCG, true>(sb, 1, g, n, x1, hout);
@@ -278,17 +289,22 @@ __device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, 
 // it spilled 4-28k VGPRs).  op_next: 0 after the output layer.
 template <int NCG>
 __device__ __forceinline__ void net_layer(NetStream &ws, int nch, int op_next, int g, int n,
-                                          float *sa, float *sb, net_f4 (&hin)[16], net_f4 (&hout)[16]) {
+                                          float *sa, float *sb, bool active, net_f4 (&hin)[16],
+                                          net_f4 (&hout)[16]) {
     constexpr int op = 64 * NCG;
     for (int lc = 0; lc < nch; lc += 2) {
         net_chunk_wait();
         net_issue(ws, op, sb);                              // lc + 1 < nch: nch is even
-        net_half_mm<NCG, false>(sa, 0, g, n, hin[0], hout);
-        net_half_mm<NCG, false>(sa, 1, g, n, hin[1], hout);
+        if (active) {
+            net_half_mm<NCG, false>(sa, 0, g, n, hin[0], hout);
+            net_half_mm<NCG, false>(sa, 1, g, n, hin[1], hout);
+        }
         net_chunk_wait();
         net_issue(ws, lc + 2 < nch ? op : op_next, sa);
-        net_half_mm<NCG, false>(sb, 0, g, n, hin[2], hout);
-        net_half_mm<NCG, false>(sb, 1, g, n, hin[3], hout);
+        if (active) {
+            net_half_mm<NCG, false>(sb, 0, g, n, hin[2], hout);
+            net_half_mm<NCG, false>(sb, 1, g, n, hin[3], hout);
+        }
 #pragma unroll
         for (int i = 0; i < 12; ++i) hin[i] = hin[i + 4];
     }
@@ -305,8 +321,8 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     __shared__ __attribute__((aligned(16))) float slot_a[kNetSlotFloats];
     __shared__ __attribute__((aligned(16))) float slot_b[kNetSlotFloats];
     __shared__ __attribute__((aligned(16))) float sbias[kNetMaxBias];
-    __shared__ double red_loss[2][kNetFwdWaves];
-    __shared__ int red_hits[2][kNetFwdWaves];
+    __shared__ double red_loss[kNetFwdWaves];
+    __shared__ int red_hits[kNetFwdWaves];
 
     // XCD-aware: blocks b and b + 8 share an XCD (MI355X_MICROARCH), so the T
     // row tiles of one env are consecutive on ONE XCD and its L2 serves the
@@ -318,18 +334,17 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63, g = lane >> 4, n = lane & 15;
     const int row = tile * kNetTile + wave * kNetWaveRows + n;
-    const bool rvalid = row < a.N;
+    const bool rvalid = row < a.rows;
+    // a wave without a valid row (the minibatch's last tile) keeps the DMA
+    // and barriers but issues no MFMA: its SIMD serves the other workgroup
+    const bool active = tile * kNetTile + wave * kNetWaveRows < a.rows;
     const float *img = a.img + static_cast<size_t>(e) * a.g.Pimg;
     const int nl = a.g.nl;
     NetStream ws{img, wave, lane};
 
     for (int i = tid; i < a.g.bias_total; i += kNetThreads) sbias[i] = img[a.g.bias_base + i];
-    int slot_n = -1;
-    int yl = 0;
-    if (rvalid) {
-        slot_n = a.mb_slot ? a.mb_slot[static_cast<size_t>(e) * a.N + row] : row;
-        yl = a.label[row];
-    }
+    const int slot_n = a.mb && rvalid ? row : -1;
+    const int yl = rvalid ? a.label[e * a.label_env + row] : 0;
 
     net_f4 hin[16], hout[16];
     auto bias_init = [&](int l, int ncg) {
@@ -350,8 +365,9 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     // ---- layer 0: K = the input features, B operand = X rows
     // (this wave's 16-row block of Xt, the lane's float4 of feature group 0)
     net_layer0<NCGH>(ws, a.g.nchunk[0], op_of(1), a.F16,
-                     a.Xt + (static_cast<size_t>(tile * (kNetTile / 16) + wave) * a.F16 * 64 + lane) * 4,
-                     g, n, slot_a, slot_b, hout);
+                     a.Xt + e * a.xt_env +
+                         (static_cast<size_t>(tile * (kNetTile / 16) + wave) * a.F16 * 64 + lane) * 4,
+                     g, n, slot_a, slot_b, active, hout);
 
     // ---- layers 1 .. nl-1: K = the previous layer's units, from registers
     for (int l = 0; l + 1 < nl; ++l) {
@@ -364,7 +380,7 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) hin[c * 4 + j][i] = fmaxf(hout[c * 4 + j][i], 0.0f);
         if (slot_n >= 0) {
-            float *dst = a.act_mb[l] + (static_cast<size_t>(e) * a.B + slot_n) * OPH;
+            float *dst = a.act_mb[l] + (static_cast<size_t>(e) * a.rows + slot_n) * OPH;   // mb mode: rows = B
 #pragma unroll
             for (int c = 0; c < NCGH; ++c)
 #pragma unroll
@@ -374,11 +390,11 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
         }
         if (l + 2 < nl) {
             bias_init(l + 1, NCGH);
-            net_layer<NCGH>(ws, 2 * NCGH, op_of(l + 2), g, n, slot_a, slot_b, hin, hout);
+            net_layer<NCGH>(ws, 2 * NCGH, op_of(l + 2), g, n, slot_a, slot_b, active, hin, hout);
         }
     }
     bias_init(nl - 1, 1);
-    net_layer<1>(ws, 2 * NCGH, 0, g, n, slot_a, slot_b, hin, hout);   // the output layer
+    net_layer<1>(ws, 2 * NCGH, 0, g, n, slot_a, slot_b, active, hin, hout);   // the output layer
 
     // ---- logits -> softmax (utils_math.py:51-63), -log(p_y + 1e-16)
     // (utils_math.py:25-34), np.argmax's first maximum of P; class 16g + 4i + j
@@ -422,39 +438,78 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
         loss_r = static_cast<double>(-logf(py + 1e-16f));
         hit_r = arg == yl ? 1 : 0;
         if (slot_n >= 0) {
-            float *dz = a.dz_out + (static_cast<size_t>(e) * a.B + slot_n) * 64;   // output op = 64
+            float *dz = a.dz_out + (static_cast<size_t>(e) * a.rows + slot_n) * 64;   // output op = 64
 #pragma unroll
             for (int k = 0; k < kNetMaxClasses; ++k)
                 if (k < K) dz[k] = z[k] - (k == yl ? 1.0f : 0.0f);
         }
     }
-    double lsum[2] = {loss_r, slot_n >= 0 ? loss_r : 0.0};
-    int hsum[2] = {hit_r, slot_n >= 0 ? hit_r : 0};
+    double lsum = loss_r;
+    int hsum = hit_r;
 #pragma unroll
-    for (int w = 8; w > 0; w >>= 1)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            lsum[s] += __shfl_xor(lsum[s], w);
-            hsum[s] += __shfl_xor(hsum[s], w);
-        }
-    if (lane == 0)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            red_loss[s][wave] = lsum[s];
-            red_hits[s][wave] = hsum[s];
-        }
+    for (int w = 8; w > 0; w >>= 1) {
+        lsum += __shfl_xor(lsum, w);
+        hsum += __shfl_xor(hsum, w);
+    }
+    if (lane == 0) {
+        red_loss[wave] = lsum;
+        red_hits[wave] = hsum;
+    }
     __syncthreads();
-    if (tid < 2) {
+    if (tid == 0) {
         double l = 0.0;
         int h = 0;
 #pragma unroll
         for (int w = 0; w < kNetFwdWaves; ++w) {
-            l += red_loss[tid][w];
-            h += red_hits[tid][w];
+            l += red_loss[w];
+            h += red_hits[w];
         }
-        const size_t o = (static_cast<size_t>(e) * a.T + tile) * 2 + tid;
+        const size_t o = static_cast<size_t>(e) * a.T + tile;
         a.part_loss[o] = l;
         a.part_hits[o] = h;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The minibatch rows of env e -- dataset row order[sel][e][i] for slot
+// i < B (optimize.py:72-76: sequence[0] of the env's row order) -- in the
+// forward's B-operand layout (lane g * 16 + n of 16-row block rb, feature
+// group t holds row 16 rb + n's features 16 t + 4 g .. + 3; zeros past F and
+// past B), with their labels.  One workgroup per 16-row block.
+struct NetGatherArgs {
+    int E, N, B, F, F16, Tmb;
+    const float *X;                  // [N][F]
+    const int32_t *label;            // [N]
+    const int32_t *order;            // [2][E][N] (nullptr: rows in order)
+    const int32_t *order_sel;
+    float *Xmb;                      // [E][Tmb * 4][F16][64][4]
+    int32_t *label_mb;               // [E][Tmb * 64]
+};
+
+__global__ __launch_bounds__(kNetThreads) void net_gather_kernel(NetGatherArgs a) {
+    const int e = blockIdx.y, rb = blockIdx.x;
+    __shared__ int32_t src[16];
+    if (threadIdx.x < 16) {
+        const int i = rb * 16 + threadIdx.x;
+        int32_t r = -1;
+        if (i < a.B)
+            r = a.order ? a.order[(static_cast<size_t>(a.order_sel[e]) * a.E + e) * a.N + i] : i;
+        src[threadIdx.x] = r;
+        a.label_mb[static_cast<size_t>(e) * a.Tmb * 64 + i] = r >= 0 ? a.label[r] : 0;
+    }
+    __syncthreads();
+    float *dst = a.Xmb + ((static_cast<size_t>(e) * a.Tmb * 4 + rb) * a.F16) * 256;
+    for (int q = threadIdx.x; q < a.F16 * 64; q += kNetThreads) {
+        const int t = q >> 6, ln = q & 63;
+        const int32_t r = src[ln & 15];
+        const int f0 = 16 * t + 4 * (ln >> 4);
+        net_f4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (r >= 0) {
+            const float *x = a.X + static_cast<size_t>(r) * a.F;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = f0 + c < a.F ? x[f0 + c] : 0.0f;
+        }
+        *reinterpret_cast<net_f4 *>(dst + static_cast<size_t>(q) * 4) = v;
     }
 }
 
@@ -547,6 +602,22 @@ constexpr int kNetGradBatch = 16;
 #define CE_NET_GRAD_BLOCKS 2
 #endif
 constexpr int kNetGradWaveBlocks = CE_NET_GRAD_BLOCKS;
+// CE_NET_GRAD_NT = 1: the float64 history and the observation stream with
+// nontemporal loads / stores (they are touched once per step; the forward
+// running beside this kernel re-reads its weight chunks from L2)
+#ifndef CE_NET_GRAD_NT
+#define CE_NET_GRAD_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ T net_ld_stream(const T *p) {
+    if (CE_NET_GRAD_NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <typename T>
+__device__ __forceinline__ void net_st_stream(T v, T *p) {
+    if (CE_NET_GRAD_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 constexpr int kNetGradTile = 4 * 32 * kNetGradWaveBlocks;   // units per workgroup task
 
 __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
@@ -630,7 +701,7 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {                  // clamped: every load unconditional
                 const int kk = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
-                gold[r] = G[fw + static_cast<int64_t>(kk <= din ? kk : din) * dout + uc];
+                gold[r] = net_ld_stream(&G[fw + static_cast<int64_t>(kk <= din ? kk : din) * dout + uc]);
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -639,9 +710,9 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
                 const int64_t p = fw + static_cast<int64_t>(kk) * dout + u;
                 const float gv = acc[bb][r] / fB;
                 const double gn = static_cast<double>(gv) / (fabs(gold[r]) + 1.0);
-                obs[p] = 0.0f;                              // wght_hist is identically 0
-                obs[P + 1 + p] = wipe ? 0.0f : static_cast<float>(gn);
-                G[p] = wipe ? 0.0 : gn;
+                net_st_stream(0.0f, &obs[p]);               // wght_hist is identically 0
+                net_st_stream(wipe ? 0.0f : static_cast<float>(gn), &obs[P + 1 + p]);
+                net_st_stream(wipe ? 0.0 : gn, &G[p]);
             }
         }
     }
@@ -654,10 +725,12 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
 // auto-reset: W <- W0 (the image), L, step, order <- order[perm] and the
 // minibatch slots of the new order.
 struct NetFinArgs {
-    int E, N, B, P, T, max_steps, auto_reset;
+    int E, N, B, P, T, Tmb, max_steps, auto_reset;
     int64_t Pimg;
-    const double *part_loss;
+    const double *part_loss;         // [E][T]: the info forward's tiles
     const int32_t *part_hits;
+    const double *mb_loss;           // [E][Tmb]: the minibatch forward's
+    const int32_t *mb_hits;
     float *img;
     const float *img0;
     double *L;
@@ -665,7 +738,6 @@ struct NetFinArgs {
     const int32_t *perm;
     int32_t *order;
     int32_t *order_sel;
-    int32_t *mb_slot;
     float *obs;
     float *reward;
     uint8_t *done;
@@ -675,18 +747,13 @@ struct NetFinArgs {
 };
 
 // order <- order[perm] (the reset's shuffle composed onto the current row
-// order) and the slot of every row in the new minibatch (-1 past B)
+// order)
 __device__ inline void net_compose_order(const NetFinArgs &a, int e) {
     const int sel = a.order_sel[e];
     const int32_t *cur = a.order + (static_cast<size_t>(sel) * a.E + e) * a.N;
     int32_t *nxt = a.order + (static_cast<size_t>(1 - sel) * a.E + e) * a.N;
     const int32_t *pm = a.perm + static_cast<size_t>(e) * a.N;
-    int32_t *slots = a.mb_slot + static_cast<size_t>(e) * a.N;
-    for (int i = threadIdx.x; i < a.N; i += kNetThreads) {
-        const int32_t r = cur[pm[i]];
-        nxt[i] = r;
-        slots[r] = i < a.B ? i : -1;
-    }
+    for (int i = threadIdx.x; i < a.N; i += kNetThreads) nxt[i] = cur[pm[i]];
     __syncthreads();
     if (threadIdx.x == 0) a.order_sel[e] = 1 - sel;
 }
@@ -701,11 +768,12 @@ __global__ __launch_bounds__(kNetThreads) void net_finish_kernel(NetFinArgs a) {
         double lm = 0.0, li = 0.0;
         int hm = 0, hi = 0;
         for (int t = 0; t < a.T; ++t) {
-            const size_t o = (static_cast<size_t>(e) * a.T + t) * 2;
-            li += a.part_loss[o];
-            lm += a.part_loss[o + 1];
-            hi += a.part_hits[o];
-            hm += a.part_hits[o + 1];
+            li += a.part_loss[static_cast<size_t>(e) * a.T + t];
+            hi += a.part_hits[static_cast<size_t>(e) * a.T + t];
+        }
+        for (int t = 0; t < a.Tmb; ++t) {
+            lm += a.mb_loss[static_cast<size_t>(e) * a.Tmb + t];
+            hm += a.mb_hits[static_cast<size_t>(e) * a.Tmb + t];
         }
         // the loss is a float32 mean in the reference (TF / numpy float32)
         const float loss = static_cast<float>(lm / a.B);
@@ -759,7 +827,7 @@ __global__ __launch_bounds__(kNetThreads) void net_reset_params_kernel(NetResetA
     for (size_t i = t0; i < n4; i += st) w[i] = w0[i];
 }
 
-// per env: L, step, and order <- order[perm] with its minibatch slots
+// per env: L, step, and order <- order[perm]
 __global__ __launch_bounds__(kNetThreads) void net_reset_env_kernel(NetFinArgs a) {
     const int e = blockIdx.x;
     if (threadIdx.x == 0) {
@@ -767,14 +835,6 @@ __global__ __launch_bounds__(kNetThreads) void net_reset_env_kernel(NetFinArgs a
         a.step[e] = 0;
     }
     if (a.order != nullptr) net_compose_order(a, e);
-}
-
-// minibatch slots of the current row order (after ce_set_state wrote one)
-__global__ __launch_bounds__(kNetThreads) void net_slots_kernel(NetFinArgs a) {
-    const int e = blockIdx.x;
-    const int32_t *cur = a.order + (static_cast<size_t>(a.order_sel[e]) * a.E + e) * a.N;
-    int32_t *slots = a.mb_slot + static_cast<size_t>(e) * a.N;
-    for (int i = threadIdx.x; i < a.N; i += kNetThreads) slots[cur[i]] = i < a.B ? i : -1;
 }
 
 }  // namespace ce
