@@ -121,14 +121,14 @@ struct NetPlan {
     double *mb_loss = nullptr;               // [E][Tmb]: minibatch forward (B < N)
     int32_t *mb_hits = nullptr;
     hipStream_t side = nullptr;              // the gradient chain
-    hipStream_t fwd = nullptr;               // the info forward
-    hipEvent_t fork = nullptr, join = nullptr, fwd_done = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     float *act_mb[kNetL] = {nullptr};        // hidden l: [E][B][op_l]
     float *dz_mb[kNetL] = {nullptr};         // hidden l: [E][B][op_l]
     float *dz_out = nullptr;                 // [E][B][op_{nl-1}]
     int task0[kNetL + 1] = {0};
     int ut[kNetL] = {0};
-    int tpe = 0;                             // net_grad_kernel workgroups per env
+    int tpe = 0;                             // net_grad_kernel tasks per env
+    int cus = 256;                           // compute units (the persistent grad grid)
     int upd_blocks = 0;
 };
 
@@ -199,18 +199,12 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
     }
     if ((rc = dev_alloc(&p->part_loss, E * p->T, true)) != CE_OK) return bail(rc);
     if ((rc = dev_alloc(&p->part_hits, E * p->T, true)) != CE_OK) return bail(rc);
-    // CE_NET_SIDE_PRIO = 1: the info forward on a stream of the greatest
-    // priority, so a slot the forward frees goes to its next workgroup before
-    // the gradient chain's
-#ifndef CE_NET_SIDE_PRIO
-#define CE_NET_SIDE_PRIO 0
-#endif
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    if (hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-        hipStreamCreateWithPriority(&p->fwd, hipStreamNonBlocking, CE_NET_SIDE_PRIO ? prio_hi : prio_lo) !=
-            hipSuccess ||
-        hipEventCreateWithFlags(&p->fwd_done, hipEventDisableTiming) != hipSuccess ||
+    // (stream priorities were measured: a greatest-priority stream for the
+    // forward changed nothing; the persistent grad grid is what keeps the
+    // forward's slots)
+    if (hipDeviceGetAttribute(&p->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        return bail(fail(CE_EHIP, "network: device attribute"));
+    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&p->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&p->join, hipEventDisableTiming) != hipSuccess)
         return bail(fail(CE_EHIP, "network: side stream / events"));
@@ -245,9 +239,7 @@ void net_destroy(NetPlan *p) {
         if (b) (void)hipFree(b);
     if (p->fork) (void)hipEventDestroy(p->fork);
     if (p->join) (void)hipEventDestroy(p->join);
-    if (p->fwd_done) (void)hipEventDestroy(p->fwd_done);
     if (p->side) (void)hipStreamDestroy(p->side);
-    if (p->fwd) (void)hipStreamDestroy(p->fwd);
     for (int l = 0; l < kNetL; ++l) {
         if (p->act_mb[l]) (void)hipFree(p->act_mb[l]);
         if (p->dz_mb[l]) (void)hipFree(p->dz_mb[l]);
@@ -332,10 +324,17 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         for (int l = 0; l < kNetL; ++l) f.act_mb[l] = p->act_mb[l];
         f.dz_out = p->dz_out;
         const unsigned grid = static_cast<unsigned>((E + 7) / 8 * 8) * f.T;
-        if (g.op[0] == kNetMaxOp)
-            hipLaunchKernelGGL(net_fwd_kernel<kNetMaxOp / 64>, dim3(grid), dim3(kNetThreads), 0, st, f);
-        else
-            hipLaunchKernelGGL(net_fwd_kernel<1>, dim3(grid), dim3(kNetThreads), 0, st, f);
+        const bool narrow = g.dout[nl - 1] <= 16;
+        if (g.op[0] == kNetMaxOp) {
+            if (narrow)
+                hipLaunchKernelGGL((net_fwd_kernel<kNetMaxOp / 64, true>), dim3(grid), dim3(kNetThreads), 0, st, f);
+            else
+                hipLaunchKernelGGL((net_fwd_kernel<kNetMaxOp / 64, false>), dim3(grid), dim3(kNetThreads), 0, st, f);
+        } else if (narrow) {
+            hipLaunchKernelGGL((net_fwd_kernel<1, true>), dim3(grid), dim3(kNetThreads), 0, st, f);
+        } else {
+            hipLaunchKernelGGL((net_fwd_kernel<1, false>), dim3(grid), dim3(kNetThreads), 0, st, f);
+        }
     };
     if (split) {
         NetGatherArgs ga{};
@@ -359,10 +358,8 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
     hipStream_t gs = s;
     if (split) {
         CE_HIP(hipEventRecord(p->fork, s));
-        CE_HIP(hipStreamWaitEvent(p->fwd, p->fork, 0));
         CE_HIP(hipStreamWaitEvent(p->side, p->fork, 0));
-        forward(false, p->fwd);                             // first: it takes its 2 workgroups per CU
-        CE_HIP(hipEventRecord(p->fwd_done, p->fwd));
+        forward(false, s);                                  // first: it takes its 2 workgroups per CU
         gs = p->side;
     }
     for (int lh = nl - 2; lh >= 0; --lh) {
@@ -401,12 +398,15 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         r.step = a.step;
         r.G = a.G;
         r.obs = a.obs;
-        hipLaunchKernelGGL(net_grad_kernel, dim3(std::min(p->tpe, kNetGradBlocks), E), dim3(kNetThreads),
-                           0, gs, r);
+        // beside the forward: one workgroup per CU; alone: 8 per env
+#ifndef CE_NET_GRAD_PER_CU
+#define CE_NET_GRAD_PER_CU 1
+#endif
+        const int grid = split ? CE_NET_GRAD_PER_CU * p->cus : 8 * std::min(p->tpe, kNetGradBlocks) * ((E + 7) / 8);
+        hipLaunchKernelGGL(net_grad_kernel, dim3((grid + 7) / 8 * 8), dim3(kNetThreads), 0, gs, r);
     }
     if (split) {
         CE_HIP(hipEventRecord(p->join, p->side));
-        CE_HIP(hipStreamWaitEvent(s, p->fwd_done, 0));
         CE_HIP(hipStreamWaitEvent(s, p->join, 0));
     }
     hipLaunchKernelGGL(net_finish_kernel, dim3(E), dim3(kNetThreads), 0, s, fin_args(p, a));

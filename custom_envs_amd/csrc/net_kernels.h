@@ -266,9 +266,11 @@ __device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, 
         net_f4 x0 = xn[0], x1 = xn[1];
         net_issue(ws, op_at(lc + 1), sb);
         if (lc + 1 < nch) xload(lc + 1);
+        // (a chunk half past the features -- F = 784 fills 24.5 chunks -- is
+        // zero rows times zero features: skipped)
         if (active) {
             net_half_mm<NCG, true>(sa, 0, g, n, x0, hout);
-            net_half_mm<NCG, true>(sa, 1, g, n, x1, hout);
+            if (2 * lc + 1 < F16) net_half_mm<NCG, true>(sa, 1, g, n, x1, hout);
         }
         net_chunk_wait();
         x0 = xn[0];
@@ -277,7 +279,7 @@ __device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, 
         if (lc + 1 < nch && active) {                       // not the padding chunk
             if (lc + 2 < nch) xload(lc + 2);
             net_half_mm<NCG, true>(sb, 0, g, n, x0, hout);
-            net_half_mm<NCG, true>(sb, 1, g, n, x1, hout);
+            if (2 * lc + 3 < F16) net_half_mm<NCG, true>(sb, 1, g, n, x1, hout);
         }
     }
 }
@@ -310,12 +312,47 @@ __device__ __forceinline__ void net_layer(NetStream &ws, int nch, int op_next, i
     }
 }
 
+// The output layer for K <= 16 classes ("narrow"): one MFMA block per K step
+// instead of four.  The lane's A operand is the scalar at column n of image
+// row 16 s + 4 k + g (unit n: the image keeps its 64-column layout), so block
+// lane (g, n) register i ends as unit 4 g + i of row n; the four-block form
+// computed 64 units for <= 16 real ones (5 % of the forward's MFMAs).
+__device__ __forceinline__ void net_half_mm_narrow(const float *sl, int s, int g, int n, const net_f4 &bv,
+                                                   net_f4 &h0) {
+    float w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = sl[(16 * s + 4 * k + g) * 64 + n];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h0 = net_mfma16(w[k], bv[k], h0);
+}
+
+__device__ __forceinline__ void net_layer_narrow(NetStream &ws, int nch, int g, int n, float *sa, float *sb,
+                                                 bool active, net_f4 (&hin)[16], net_f4 &h0) {
+    for (int lc = 0; lc < nch; lc += 2) {
+        net_chunk_wait();
+        net_issue(ws, 64, sb);                              // lc + 1 < nch: nch is even
+        if (active) {
+            net_half_mm_narrow(sa, 0, g, n, hin[0], h0);
+            net_half_mm_narrow(sa, 1, g, n, hin[1], h0);
+        }
+        net_chunk_wait();
+        if (lc + 2 < nch) net_issue(ws, 64, sa);
+        if (active) {
+            net_half_mm_narrow(sb, 0, g, n, hin[2], h0);
+            net_half_mm_narrow(sb, 1, g, n, hin[3], h0);
+        }
+#pragma unroll
+        for (int i = 0; i < 12; ++i) hin[i] = hin[i + 4];
+    }
+}
+
 // NCGH: 64-unit output groups of every hidden layer (net_geometry pads all
 // hidden widths to one op = 64 NCGH, 64 or 256); the output layer has one
 // (K <= 32).  So layer l's op, chunk count and bias offset are static
 // functions of l: op = 64 NCGH (hidden) / 64 (output), nchunk = 2 NCGH
 // (l >= 1), bias at l * 64 NCGH.
-template <int NCGH>
+// NARROW: the output layer has <= 16 classes (net_layer_narrow)
+template <int NCGH, bool NARROW>
 __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     constexpr int OPH = 64 * NCGH;
     __shared__ __attribute__((aligned(16))) float slot_a[kNetSlotFloats];
@@ -393,21 +430,36 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
             net_layer<NCGH>(ws, 2 * NCGH, op_of(l + 2), g, n, slot_a, slot_b, active, hin, hout);
         }
     }
-    bias_init(nl - 1, 1);
-    net_layer<1>(ws, 2 * NCGH, 0, g, n, slot_a, slot_b, active, hin, hout);   // the output layer
-
-    // ---- logits -> softmax (utils_math.py:51-63), -log(p_y + 1e-16)
-    // (utils_math.py:25-34), np.argmax's first maximum of P; class 16g + 4i + j
-    // of row n sits in lane group g, so lane group 0 gathers the row
     const int K = a.g.dout[nl - 1];
     float z[kNetMaxClasses];
+    if (NARROW) {
+        // bias of unit 4 g + i: permuted slot 16 i + g of the layer (net_bias_slot)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) hout[0][i] = sbias[(nl - 1) * OPH + 16 * i + g];
+        net_layer_narrow(ws, 2 * NCGH, g, n, slot_a, slot_b, active, hin, hout[0]);
+        // class 4 g' + i of row n sits in lane 16 g' + n, register i
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            z[4 * i + j] = hout[j][i];
-            z[16 + 4 * i + j] = __shfl_down(hout[j][i], 16);
-        }
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int gp = 0; gp < 4; ++gp) z[4 * gp + i] = __shfl(hout[0][i], 16 * gp + n);
+#pragma unroll
+        for (int k = 16; k < kNetMaxClasses; ++k) z[k] = 0.0f;
+    } else {
+        bias_init(nl - 1, 1);
+        net_layer<1>(ws, 2 * NCGH, 0, g, n, slot_a, slot_b, active, hin, hout);   // the output layer
+        // class 16g + 4i + j of row n sits in lane group g: lane group 0
+        // gathers the row
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                z[4 * i + j] = hout[j][i];
+                z[16 + 4 * i + j] = __shfl_down(hout[j][i], 16);
+            }
+    }
+
+    // ---- logits -> softmax (utils_math.py:51-63), -log(p_y + 1e-16)
+    // (utils_math.py:25-34), np.argmax's first maximum of P, in lane group 0
     double loss_r = 0.0;
     int hit_r = 0;
     const bool owner = g == 0 && rvalid;
@@ -588,6 +640,14 @@ struct NetGradArgs {
     float *obs;                      // [E][2P + 1]
 };
 
+typedef uint32_t net_u2 __attribute__((ext_vector_type(2)));
+
+// A raw buffer resource over [p, p + bytes): 32-bit offsets, and an access
+// at or past `bytes` is dropped (store) or reads 0 (load) in hardware
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t net_rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, static_cast<int>(bytes), 0x00020000);
+}
+
 __device__ __forceinline__ net_f16 net_mfma32(float a, float b, net_f16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -602,37 +662,35 @@ constexpr int kNetGradBatch = 16;
 #define CE_NET_GRAD_BLOCKS 2
 #endif
 constexpr int kNetGradWaveBlocks = CE_NET_GRAD_BLOCKS;
-// CE_NET_GRAD_NT = 1: the float64 history and the observation stream with
-// nontemporal loads / stores (they are touched once per step; the forward
-// running beside this kernel re-reads its weight chunks from L2)
-#ifndef CE_NET_GRAD_NT
-#define CE_NET_GRAD_NT 0
-#endif
-template <typename T>
-__device__ __forceinline__ T net_ld_stream(const T *p) {
-    if (CE_NET_GRAD_NT) return __builtin_nontemporal_load(p);
-    return *p;
-}
-template <typename T>
-__device__ __forceinline__ void net_st_stream(T v, T *p) {
-    if (CE_NET_GRAD_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
 constexpr int kNetGradTile = 4 * 32 * kNetGradWaveBlocks;   // units per workgroup task
 
+// Persistent grid (a multiple of 8 workgroups): workgroup b works on XCD
+// b & 7 (MI355X_MICROARCH: round-robin dispatch) and walks that XCD's envs
+// (e = xcd + 8 j) task by task with the XCD's other workgroups, so an env's
+// minibatch activations are pulled into ONE L2.  Beside the forward the grid
+// is one workgroup per CU: it fits in the VGPRs the forward's two workgroups
+// leave and never holds a slot the forward's next workgroup needs.
 __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
-    const int e = blockIdx.y;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, h = lane >> 5, m = lane & 31;
     const int nl = a.g.nl;
-    const int cur = a.step[e];
-    const bool wipe = cur >= a.max_steps && a.auto_reset;
+    const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
+    const int n_env = a.E > xcd ? (a.E - xcd + 7) >> 3 : 0;       // this XCD's envs
     const float fB = static_cast<float>(a.B);
+    // g / B: a power-of-two B divides exactly by its reciprocal (one multiply
+    // instead of the ten-instruction IEEE division sequence; this kernel runs
+    // beside the MFMA-bound forward, whose SIMDs its VALU work shares)
+    const bool pow2 = (a.B & (a.B - 1)) == 0;
+    const float rB = 1.0f / fB;
     const size_t P = a.P;
-    double *G = a.G + static_cast<size_t>(e) * P;
-    float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
-    const int32_t *rows = a.order ? a.order + (static_cast<size_t>(a.order_sel[e]) * a.E + e) * a.N : nullptr;
-    for (int task = blockIdx.x; task < a.tpe; task += gridDim.x) {
+    for (int q = blockIdx.x >> 3; q < n_env * a.tpe; q += per_xcd) {
+        const int j = q / a.tpe, task = q - j * a.tpe;
+        const int e = xcd + 8 * j;
+        const bool wipe = a.step[e] >= a.max_steps && a.auto_reset;
+        double *G = a.G + static_cast<size_t>(e) * P;
+        float *obs = a.obs + static_cast<size_t>(e) * (2 * P + 1);
+        const int32_t *rows =
+            a.order ? a.order + (static_cast<size_t>(a.order_sel[e]) * a.E + e) * a.N : nullptr;
         int l = 0;
         while (l + 1 < nl && task >= a.task0[l + 1]) ++l;
         const int tl = task - a.task0[l];
@@ -692,27 +750,36 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
         // epilogue: accumulator r of lane (h, m) = row k0 + 8(r>>2) + 4h + (r&3)
         // of [dW; db], unit u0 + 32 bb + m; every G load of a block in flight
         // before its stores
+        // Raw buffer accesses over the layer's [dW; db] range: 32-bit
+        // offsets (no 64-bit address arithmetic per element), and rows past
+        // the bias row are out of range -- their loads return 0 and their
+        // stores are dropped by the hardware, so no clamps or row masks
         const int64_t fw = a.g.flat_w[l];
+        const uint32_t nb = static_cast<uint32_t>(din + 1) * dout;
+        const __amdgpu_buffer_rsrc_t rG = net_rsrc(G + fw, nb * 8);
+        const __amdgpu_buffer_rsrc_t rW = net_rsrc(obs + fw, nb * 4);
+        const __amdgpu_buffer_rsrc_t rO = net_rsrc(obs + P + 1 + fw, nb * 4);
 #pragma unroll
         for (int bb = 0; bb < kNetGradWaveBlocks; ++bb) {
             const int u = u0 + 32 * bb + m;
+            if (u >= dout) continue;                        // per lane, once per block
+            const int base = (k0 + 4 * h) * dout + u;
             double gold[16];
-            const int uc = u < dout ? u : dout - 1;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {                  // clamped: every load unconditional
-                const int kk = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
-                gold[r] = net_ld_stream(&G[fw + static_cast<int64_t>(kk <= din ? kk : din) * dout + uc]);
+            for (int r = 0; r < 16; ++r) {
+                const int o = base + (8 * (r >> 2) + (r & 3)) * dout;
+                gold[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rG, o * 8, 0, 0));
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int kk = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
-                if (kk > din || u >= dout) continue;
-                const int64_t p = fw + static_cast<int64_t>(kk) * dout + u;
-                const float gv = acc[bb][r] / fB;
+                const int o = base + (8 * (r >> 2) + (r & 3)) * dout;
+                const float gv = pow2 ? acc[bb][r] * rB : acc[bb][r] / fB;
                 const double gn = static_cast<double>(gv) / (fabs(gold[r]) + 1.0);
-                net_st_stream(0.0f, &obs[p]);               // wght_hist is identically 0
-                net_st_stream(wipe ? 0.0f : static_cast<float>(gn), &obs[P + 1 + p]);
-                net_st_stream(wipe ? 0.0 : gn, &G[p]);
+                // wght_hist is identically 0
+                __builtin_amdgcn_raw_buffer_store_b32(0u, rW, o * 4, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    __builtin_bit_cast(uint32_t, wipe ? 0.0f : static_cast<float>(gn)), rO, o * 4, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(net_u2, wipe ? 0.0 : gn), rG, o * 8, 0, 0);
             }
         }
     }

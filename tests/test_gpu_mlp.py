@@ -493,6 +493,22 @@ def test_network_shapes(hidden, batch_size, monkeypatch):
         eng.close()
 
 
+@pytest.mark.parametrize('n_classes', [16, 17, 32])
+def test_network_class_counts(n_classes):
+    """The output layer's two forward forms at their boundary: up to 16
+    classes one MFMA block per K step (net_layer_narrow, the softmax
+    gathering class 4g + i from lane group g), 17 to 32 the four-block form
+    -- 3 envs, 41 steps across an auto-reset."""
+    from oracle.gen_golden import mlp_dataset
+    features, targets = mlp_dataset(n_rows=192, n_features=40, n_classes=n_classes)
+    eng = _net_engine(features, targets, 3, (64, 48), 24)
+    try:
+        assert eng.step_kernel.endswith(':mfma')
+        _net_check(features, targets, eng, (64, 48), 24, [4, 5, 6], 41, scale=3e-3)
+    finally:
+        eng.close()
+
+
 def test_network_full_batch_and_depth():
     """The default network with the full batch (B = N: every row is a
     minibatch row, the info numbers are the minibatch's), and three hidden
