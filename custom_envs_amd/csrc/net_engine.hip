@@ -286,7 +286,15 @@ NetFinArgs fin_args(const NetPlan *p, const NetArgs &a) {
 int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
     const NetGeom &g = p->g;
     const int E = a.E, nl = g.nl;
-    {
+    const bool split = p->Tmb > 0;                          // B < N: a separate minibatch forward
+    // B <= 32 (the minibatch in waves 0-1): the update rides in the minibatch
+    // forward's producer waves (net_producer) -- one kernel instead of the
+    // update, the gather and the minibatch forward
+#ifndef CE_NET_FUSED
+#define CE_NET_FUSED 1
+#endif
+    const bool fused = CE_NET_FUSED && split && a.B <= 2 * kNetWaveRows;
+    if (!fused) {
         NetUpdArgs u{};
         u.g = g;
         u.E = E;
@@ -296,7 +304,6 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         u.step = a.step;
         hipLaunchKernelGGL(net_update_kernel, dim3(p->upd_blocks, E), dim3(kNetThreads), 0, s, u);
     }
-    const bool split = p->Tmb > 0;                          // B < N: a separate minibatch forward
     auto forward = [&](bool mb, hipStream_t st) {
         NetFwdArgs f{};
         f.g = g;
@@ -323,20 +330,41 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         f.mb = mb ? 1 : 0;
         for (int l = 0; l < kNetL; ++l) f.act_mb[l] = p->act_mb[l];
         f.dz_out = p->dz_out;
+        const bool fu = mb && fused;
+        if (fu) {
+            f.label = a.label;                              // indexed by the dataset row
+            f.N = a.N;
+            f.F = a.F;
+            f.P = a.P;
+            f.X = a.X;
+            f.act = a.act;
+            f.step = a.step;
+            f.order = a.order;
+            f.order_sel = a.order_sel;
+        }
         const unsigned grid = static_cast<unsigned>((E + 7) / 8 * 8) * f.T;
         const bool narrow = g.dout[nl - 1] <= 16;
+        constexpr int W4 = kNetMaxOp / 64;
+#define CE_NET_FWD(NCGH, NARROW, FU) \
+    hipLaunchKernelGGL((net_fwd_kernel<NCGH, NARROW, FU>), dim3(grid), dim3(kNetThreads), 0, st, f)
         if (g.op[0] == kNetMaxOp) {
-            if (narrow)
-                hipLaunchKernelGGL((net_fwd_kernel<kNetMaxOp / 64, true>), dim3(grid), dim3(kNetThreads), 0, st, f);
-            else
-                hipLaunchKernelGGL((net_fwd_kernel<kNetMaxOp / 64, false>), dim3(grid), dim3(kNetThreads), 0, st, f);
+            if (narrow) {
+                if (fu) CE_NET_FWD(W4, true, true);
+                else CE_NET_FWD(W4, true, false);
+            } else {
+                if (fu) CE_NET_FWD(W4, false, true);
+                else CE_NET_FWD(W4, false, false);
+            }
         } else if (narrow) {
-            hipLaunchKernelGGL((net_fwd_kernel<1, true>), dim3(grid), dim3(kNetThreads), 0, st, f);
+            if (fu) CE_NET_FWD(1, true, true);
+            else CE_NET_FWD(1, true, false);
         } else {
-            hipLaunchKernelGGL((net_fwd_kernel<1, false>), dim3(grid), dim3(kNetThreads), 0, st, f);
+            if (fu) CE_NET_FWD(1, false, true);
+            else CE_NET_FWD(1, false, false);
         }
+#undef CE_NET_FWD
     };
-    if (split) {
+    if (split && !fused) {
         NetGatherArgs ga{};
         ga.E = E;
         ga.N = a.N;

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kNetThreads) void net_update_kernel(NetUpdArgs a) {
 struct NetFwdArgs {
     NetGeom g;
     int E, rows, T, F16, mb;
-    const float *img;                // [E][Pimg]
+    float *img;                      // [E][Pimg] (FUSED writes W')
     const float *Xt;                 // [T * 4][F16][64 lanes][4]: rows in B-operand order
     int64_t xt_env;                  // floats between envs' Xt (0: shared)
     const int32_t *label;            // [T * 64] per env
@@ -168,6 +168,13 @@ struct NetFwdArgs {
     int32_t *part_hits;              // [E][T]
     float *act_mb[kNetL];            // hidden layer l: [E][B][op_l] post-relu minibatch rows
     float *dz_out;                   // [E][B][op_{nl-1}] P - Y of the minibatch rows
+    // FUSED only: the update's action and the minibatch rows
+    int N, F, P;
+    const float *X;                  // [N][F]
+    const float *act;                // [E][P] flat
+    int32_t *step;
+    const int32_t *order;            // [2][E][N] (nullptr: rows in order)
+    const int32_t *order_sel;
 };
 
 __device__ __forceinline__ net_f4 net_mfma16(float a, float b, net_f4 c) {
@@ -216,12 +223,13 @@ __device__ __forceinline__ void net_half_mm(const float *sl, int s, int g, int n
 struct NetStream {
     const float *next;               // source of the next chunk to load
     int wave, lane;
+    bool dma;                        // false: producer waves fill the slots (FUSED)
 };
 
 // LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction) of the next
 // chunk (32 rows x op floats) into dst; op == 0: nothing to load
 __device__ __forceinline__ void net_issue(NetStream &ws, int op, float *dst) {
-    if (op == 0) return;
+    if (op == 0 || !ws.dma) return;
     const int ninst = op >> 3;
     for (int k = ws.wave; k < ninst; k += kNetFwdWaves)
         __builtin_amdgcn_global_load_lds(
@@ -243,10 +251,11 @@ __device__ __forceinline__ void net_chunk_wait() {
 // Layer 0 over its nch chunks, padded to even (slot A for even positions, B
 // for odd): B operands from the Xt image, prefetched a chunk ahead.
 // op_next: width of the next layer's chunks (loaded once this layer's are).
-template <int NCG>
-__device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, int F16,
-                                           const float *xt, int g, int n, float *sa, float *sb,
-                                           bool active, net_f4 (&hout)[16]) {
+// xf(t): the lane's float4 of feature group t (t < F16).
+template <int NCG, typename XF>
+__device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, int F16, const XF &xf,
+                                           int g, int n, float *sa, float *sb, bool active,
+                                           net_f4 (&hout)[16]) {
     constexpr int op = 64 * NCG;
     // what position q of the padded sequence loads: a real chunk, the padding
     // (nothing), or the next layer's first chunk
@@ -254,9 +263,7 @@ __device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, 
     net_f4 xn[2];
     auto xload = [&](int lc) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-            xn[t] = 2 * lc + t < F16 ? *reinterpret_cast<const net_f4 *>(xt + (2 * lc + t) * 256)
-                                     : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int t = 0; t < 2; ++t) xn[t] = 2 * lc + t < F16 ? xf(2 * lc + t) : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
     };
     xload(0);
     // the X operands are copied out before the next DMA issues (vmcnt counts
@@ -346,13 +353,117 @@ __device__ __forceinline__ void net_layer_narrow(NetStream &ws, int nch, int g, 
     }
 }
 
+// FUSED mode's producer waves (2 and 3; the minibatch's <= 32 rows are waves
+// 0 and 1): the update W' = W - a (optimize.py:74-75, as net_update_kernel)
+// streamed chunk by chunk through registers -- W' to the env's image in HBM
+// and into the LDS slot the consumer waves multiply next.  The barrier
+// schedule is the consumers': the sbias barrier, one per chunk position of
+// the stream (layer 0's count padded to even), and the partials' barrier.
+// After barrier p the slot of chunk p - 1 is free: chunk p + 1 goes there and
+// chunk p + 2's loads are issued, a whole chunk of consumer work ahead.
+template <int NCGH>
+__device__ __forceinline__ void net_producer(const NetFwdArgs &a, int e, int pw, int lane, float *slot_a,
+                                             float *slot_b, float *sbias, double *red_loss, int *red_hits) {
+    constexpr int OPH = 64 * NCGH;
+    constexpr int R = kNetChunk / 2;                        // rows per producer wave and chunk
+    const int nl = a.g.nl;
+    float *img = a.img + static_cast<size_t>(e) * a.g.Pimg;
+    const float *act = a.act + static_cast<size_t>(e) * a.P;
+    // the bias area (slot s of layer l's block is unit net_bias_unit(s))
+    for (int s4 = (pw * 64 + lane) * 4; s4 < a.g.bias_total; s4 += 128 * 4) {
+        net_f4 w = *reinterpret_cast<const net_f4 *>(img + a.g.bias_base + s4);
+#pragma unroll
+        for (int l = 0; l < kNetL; ++l) {
+            if (l >= nl) break;
+            const int rel = s4 - a.g.bias_rel[l];
+            if (rel < 0 || rel >= a.g.op[l]) continue;
+            const float *b = act + a.g.flat_w[l] + static_cast<int64_t>(a.g.din[l]) * a.g.dout[l];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int un = net_bias_unit(rel + c);
+                if (un < a.g.dout[l]) w[c] -= b[un];
+            }
+        }
+        *reinterpret_cast<net_f4 *>(img + a.g.bias_base + s4) = w;
+        *reinterpret_cast<net_f4 *>(sbias + s4) = w;
+    }
+    const int nch0 = a.g.nchunk[0], p0 = nch0 + (nch0 & 1);
+    const int np = p0 + (nl - 1) * 2 * NCGH;
+    net_f4 wv[R];
+    float av[R][4];
+    // chunk position p -> layer, chunk (false: layer 0's padding or the end)
+    auto locate = [&](int p, int &l, int &c) {
+        if (p < p0) {
+            l = 0;
+            c = p;
+            return p < nch0;
+        }
+        l = 1 + (p - p0) / (2 * NCGH);
+        c = (p - p0) % (2 * NCGH);
+        return p < np;
+    };
+    auto load = [&](int p) {
+        int l, c;
+        if (!locate(p, l, c)) return;
+        const int op = l == nl - 1 ? 64 : OPH, din = a.g.din[l], dout = a.g.dout[l];
+        const float *src = img + a.g.img_off[l] + static_cast<int64_t>(c) * kNetChunk * op;
+        const float *al = act + a.g.flat_w[l];
+        const int v = 4 * lane;
+        const bool wok = v < op;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int rho = pw + 2 * i, k = net_row_unit(l, c * kNetChunk + rho);
+            wv[i] = wok ? *reinterpret_cast<const net_f4 *>(src + rho * op + v) : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
+            const float *ar = al + static_cast<int64_t>(k < din ? k : 0) * dout;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) av[i][q] = k < din && v + q < dout ? ar[v + q] : 0.0f;
+        }
+    };
+    auto store = [&](int p, float *slot) {
+        int l, c;
+        if (!locate(p, l, c)) return;
+        const int op = l == nl - 1 ? 64 : OPH;
+        float *dst = img + a.g.img_off[l] + static_cast<int64_t>(c) * kNetChunk * op;
+        const int v = 4 * lane;
+        if (v >= op) return;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int rho = pw + 2 * i;
+            const net_f4 w = {wv[i][0] - av[i][0], wv[i][1] - av[i][1], wv[i][2] - av[i][2], wv[i][3] - av[i][3]};
+            *reinterpret_cast<net_f4 *>(dst + rho * op + v) = w;
+            *reinterpret_cast<net_f4 *>(slot + rho * op + v) = w;
+        }
+    };
+    load(0);
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+    store(0, slot_a);
+    load(1);
+    __syncthreads();                                        // sbias + chunk 0
+    for (int p = 0; p < np; ++p) {
+        __syncthreads();                                    // the consumers' chunk p
+        __builtin_amdgcn_s_waitcnt(0x0f70);                 // chunk p + 1 is in registers
+        if ((p + 1) & 1) store(p + 1, slot_b);
+        else store(p + 1, slot_a);
+        load(p + 2);
+    }
+    if (lane == 0) {
+        red_loss[2 + pw] = 0.0;
+        red_hits[2 + pw] = 0;
+    }
+    __syncthreads();                                        // the partials
+}
+
 // NCGH: 64-unit output groups of every hidden layer (net_geometry pads all
 // hidden widths to one op = 64 NCGH, 64 or 256); the output layer has one
 // (K <= 32).  So layer l's op, chunk count and bias offset are static
 // functions of l: op = 64 NCGH (hidden) / 64 (output), nchunk = 2 NCGH
 // (l >= 1), bias at l * 64 NCGH.
-// NARROW: the output layer has <= 16 classes (net_layer_narrow)
-template <int NCGH, bool NARROW>
+// NARROW: the output layer has <= 16 classes (net_layer_narrow).
+// FUSED: the minibatch forward (rows = B <= 32, one workgroup per env) with
+// the update in its producer waves (net_producer) and the minibatch's
+// dataset rows read straight from X through the env's row order -- replaces
+// net_update_kernel, net_gather_kernel and the separate minibatch forward.
+template <int NCGH, bool NARROW, bool FUSED>
 __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     constexpr int OPH = 64 * NCGH;
     __shared__ __attribute__((aligned(16))) float slot_a[kNetSlotFloats];
@@ -377,11 +488,22 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     const bool active = tile * kNetTile + wave * kNetWaveRows < a.rows;
     const float *img = a.img + static_cast<size_t>(e) * a.g.Pimg;
     const int nl = a.g.nl;
-    NetStream ws{img, wave, lane};
+    NetStream ws{img, wave, lane, !FUSED};
 
-    for (int i = tid; i < a.g.bias_total; i += kNetThreads) sbias[i] = img[a.g.bias_base + i];
+    if (FUSED && wave >= 2) {
+        net_producer<NCGH>(a, e, wave - 2, lane, slot_a, slot_b, sbias, red_loss, red_hits);
+        return;
+    }
+    int xrow = 0;                                           // FUSED: the dataset row
+    if (FUSED) {
+        if (tid == 0) a.step[e] += 1;                       // current_step += 1 (baseenvironment.py:30-41)
+        if (rvalid)
+            xrow = a.order ? a.order[(static_cast<size_t>(a.order_sel[e]) * a.E + e) * a.N + row] : row;
+    } else {
+        for (int i = tid; i < a.g.bias_total; i += kNetThreads) sbias[i] = img[a.g.bias_base + i];
+    }
     const int slot_n = a.mb && rvalid ? row : -1;
-    const int yl = rvalid ? a.label[e * a.label_env + row] : 0;
+    const int yl = rvalid ? (FUSED ? a.label[xrow] : a.label[e * a.label_env + row]) : 0;
 
     net_f4 hin[16], hout[16];
     auto bias_init = [&](int l, int ncg) {
@@ -400,11 +522,27 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
     bias_init(0, NCGH);
 
     // ---- layer 0: K = the input features, B operand = X rows
-    // (this wave's 16-row block of Xt, the lane's float4 of feature group 0)
-    net_layer0<NCGH>(ws, a.g.nchunk[0], op_of(1), a.F16,
-                     a.Xt + e * a.xt_env +
-                         (static_cast<size_t>(tile * (kNetTile / 16) + wave) * a.F16 * 64 + lane) * 4,
-                     g, n, slot_a, slot_b, active, hout);
+    if (FUSED) {
+        // features 16 t + 4 g .. + 3 of the row, from X itself
+        const float *xr = a.X + static_cast<size_t>(xrow) * a.F;
+        const bool x4 = (a.F & 3) == 0;
+        auto xf = [&](int t) {
+            const int f0 = 16 * t + 4 * g;
+            net_f4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (!rvalid) return v;
+            if (x4 && f0 < a.F) return *reinterpret_cast<const net_f4 *>(xr + f0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = f0 + q < a.F ? xr[f0 + q] : 0.0f;
+            return v;
+        };
+        net_layer0<NCGH>(ws, a.g.nchunk[0], op_of(1), a.F16, xf, g, n, slot_a, slot_b, active, hout);
+    } else {
+        // (this wave's 16-row block of Xt, the lane's float4 of feature group t)
+        const float *xt = a.Xt + e * a.xt_env +
+                          (static_cast<size_t>(tile * (kNetTile / 16) + wave) * a.F16 * 64 + lane) * 4;
+        auto xf = [&](int t) { return *reinterpret_cast<const net_f4 *>(xt + t * 256); };
+        net_layer0<NCGH>(ws, a.g.nchunk[0], op_of(1), a.F16, xf, g, n, slot_a, slot_b, active, hout);
+    }
 
     // ---- layers 1 .. nl-1: K = the previous layer's units, from registers
     for (int l = 0; l + 1 < nl; ++l) {
