@@ -1052,12 +1052,12 @@ def net_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
         'roofline': {
             'bound': 'mfma', 'achieved': achieved, 'peak': MFMA_F32_PEAK_TFLOPS,
             'unit': 'TFLOP/s', 'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': None,
-            'kernel': 'one step = %s: net_update (W - a into the weight image) + '
-                      'net_fwd (every row, whole layer chain in 16x16x4 f32 MFMA accumulators, '
-                      'weights by LDS-DMA; the minibatch rows keep their activations, so the '
-                      'minibatch forward is not re-run) + net_bwd (dH per hidden layer) + '
-                      'net_grad ([dW; db] on 32x32x2 MFMA with the float64 G/obs epilogue '
-                      'from the accumulators) + net_finish; no BLAS library' % eng.step_kernel,
+            'kernel': 'one step = %s: net_fwd FUSED (W - a into the weight image by producer '
+                      'waves + the minibatch forward in 16x16x4 f32 MFMA accumulators), then '
+                      'concurrently net_fwd (every row, weights by LDS-DMA) on the main stream '
+                      'and net_bwd + net_grad ([dW; db] on 32x32x2 MFMA with the float64 G/obs '
+                      'epilogue from the accumulators) on a side stream, then net_finish; '
+                      'no BLAS library' % eng.step_kernel,
             'flops_per_env_step': train_f + info_f, 'info_flops_per_env_step': info_f,
             'step_ms_median': kernel_ms, 'step_ms_mean': kernel_ms_mean,
         },

@@ -426,11 +426,15 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         r.step = a.step;
         r.G = a.G;
         r.obs = a.obs;
-        // beside the forward: one workgroup per CU; alone: 8 per env
-#ifndef CE_NET_GRAD_PER_CU
-#define CE_NET_GRAD_PER_CU 1
+        // beside the forward: a fixed grid of ~0.62 workgroups per CU (one per
+        // CU is what fits beside the forward's two; fewer spreads the same
+        // traffic over the forward's whole run -- A/B in DESIGN 3.7); alone:
+        // 8 per env
+#ifndef CE_NET_GRAD_PCT
+#define CE_NET_GRAD_PCT 62
 #endif
-        const int grid = split ? CE_NET_GRAD_PER_CU * p->cus : 8 * std::min(p->tpe, kNetGradBlocks) * ((E + 7) / 8);
+        const int grid = split ? std::max(8, CE_NET_GRAD_PCT * p->cus / 100)
+                               : 8 * std::min(p->tpe, kNetGradBlocks) * ((E + 7) / 8);
         hipLaunchKernelGGL(net_grad_kernel, dim3((grid + 7) / 8 * 8), dim3(kNetThreads), 0, gs, r);
     }
     if (split) {

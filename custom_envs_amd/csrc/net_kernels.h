@@ -779,6 +779,14 @@ struct NetGradArgs {
 };
 
 typedef uint32_t net_u2 __attribute__((ext_vector_type(2)));
+// cache-policy bits of the epilogue's buffer loads / stores (build-time A/B;
+// gfx950: bit 1 = nt)
+#ifndef CE_NET_GRAD_AUX_LD
+#define CE_NET_GRAD_AUX_LD 0
+#endif
+#ifndef CE_NET_GRAD_AUX_ST
+#define CE_NET_GRAD_AUX_ST 0
+#endif
 
 // A raw buffer resource over [p, p + bytes): 32-bit offsets, and an access
 // at or past `bytes` is dropped (store) or reads 0 (load) in hardware
@@ -906,7 +914,7 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int o = base + (8 * (r >> 2) + (r & 3)) * dout;
-                gold[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rG, o * 8, 0, 0));
+                gold[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rG, o * 8, 0, CE_NET_GRAD_AUX_LD));
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -914,10 +922,11 @@ __global__ __launch_bounds__(kNetThreads) void net_grad_kernel(NetGradArgs a) {
                 const float gv = pow2 ? acc[bb][r] * rB : acc[bb][r] / fB;
                 const double gn = static_cast<double>(gv) / (fabs(gold[r]) + 1.0);
                 // wght_hist is identically 0
-                __builtin_amdgcn_raw_buffer_store_b32(0u, rW, o * 4, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(0u, rW, o * 4, 0, CE_NET_GRAD_AUX_ST);
                 __builtin_amdgcn_raw_buffer_store_b32(
-                    __builtin_bit_cast(uint32_t, wipe ? 0.0f : static_cast<float>(gn)), rO, o * 4, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(net_u2, wipe ? 0.0 : gn), rG, o * 8, 0, 0);
+                    __builtin_bit_cast(uint32_t, wipe ? 0.0f : static_cast<float>(gn)), rO, o * 4, 0, CE_NET_GRAD_AUX_ST);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(net_u2, wipe ? 0.0 : gn), rG, o * 8, 0,
+                                                      CE_NET_GRAD_AUX_ST);
             }
         }
     }
