@@ -33,7 +33,10 @@ def _counters(src, counter):
     per = collections.defaultdict(list)
     for path in sorted(glob.glob(os.path.join(src, '**', '*counter_collection.csv'), recursive=True)):
         for row in csv.DictReader(open(path)):
-            if row['Counter_Name'] == counter and 'ce::' in row['Kernel_Name']:
+            # a step's kernels: the engine's (ce::), not the one-off resets
+            # before the timed steps (an auto-reset runs inside the step)
+            if row['Counter_Name'] == counter and 'ce::' in row['Kernel_Name'] \
+                    and 'reset' not in row['Kernel_Name']:
                 per[row['Kernel_Name']].append(float(row['Counter_Value']))
     return per
 
