@@ -71,9 +71,12 @@ typedef double lr_d4 __attribute__((ext_vector_type(4)));
 //  CE_LR_OBS_STAGE the workgroup's observation block (16 envs x obs_stride
 //                 floats: line-aligned, whole lines) is assembled in LDS and
 //                 stored 16 B per lane in line order, instead of the zero,
-//                 L' and G' pieces each storing a part of every line
+//                 L' and G' pieces each storing a part of every line.  PMC
+//                 (4096 envs, profiles/r04_lr_writes.txt): writes 2.515 ->
+//                 2.105 MB per launch (algorithmic 2.10), reads 2.11 -> 2.10;
+//                 5.93-5.99 -> 6.00-6.03 us
 #ifndef CE_LR_OBS_STAGE
-#define CE_LR_OBS_STAGE 0
+#define CE_LR_OBS_STAGE 1
 #endif
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
