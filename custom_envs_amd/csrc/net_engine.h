@@ -19,7 +19,14 @@ constexpr int kNetMaxHidden = 4;
 constexpr int kNetL = kNetMaxHidden + 1;  // dense layers: hidden + the output layer
 constexpr int kNetMaxOp = 256;            // widest padded layer (hidden widths <= 256)
 constexpr int kNetMaxClasses = 32;
-constexpr int kNetChunk = 32;             // weight rows per LDS slot of the forward
+// weight rows per LDS slot of the forward (CE_NET_CHUNK: 32, or 16 for
+// three workgroups per CU; the image's row order is defined on 32-row groups
+// either way, net_img_row)
+#ifndef CE_NET_CHUNK
+#define CE_NET_CHUNK 32
+#endif
+constexpr int kNetChunk = CE_NET_CHUNK;
+static_assert(kNetChunk == 16 || kNetChunk == 32, "CE_NET_CHUNK: 16 or 32");
 
 // Shape of the network and of its per-env weight IMAGE (net_kernels.h).
 struct NetGeom {
@@ -46,7 +53,7 @@ struct NetGeom {
 __host__ __device__ inline int net_img_row(int l, int u) {
     if (l == 0) return u;
     const int c = u >> 6, w = u & 63, j = w & 3, i = (w >> 2) & 3, g = w >> 4;
-    return (2 * c + (j >> 1)) * kNetChunk + 16 * (j & 1) + 4 * i + g;
+    return (2 * c + (j >> 1)) * 32 + 16 * (j & 1) + 4 * i + g;
 }
 // inverse of net_img_row
 __host__ __device__ inline int net_row_unit(int l, int q) {

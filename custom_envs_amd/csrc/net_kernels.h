@@ -54,7 +54,9 @@ namespace ce {
 constexpr int kNetWaveRows = 16;      // dataset rows per wave (16x16x4 MFMA N)
 constexpr int kNetFwdWaves = 4;
 constexpr int kNetTile = kNetWaveRows * kNetFwdWaves;   // rows per forward workgroup
-constexpr int kNetSlotFloats = kNetChunk * kNetMaxOp;  // 32 KB
+constexpr int kNetSlotFloats = kNetChunk * kNetMaxOp;  // 32 / 16 KB
+constexpr int kNetHalves = kNetChunk / 16;              // 16-row MFMA K blocks per chunk
+constexpr int kNetFwdOcc = kNetChunk == 16 ? 3 : 2;      // forward workgroups per CU
 constexpr int kNetMaxBias = 4 * kNetMaxOp + 64;
 constexpr int kNetThreads = 256;
 
@@ -230,7 +232,7 @@ struct NetStream {
 // chunk (32 rows x op floats) into dst; op == 0: nothing to load
 __device__ __forceinline__ void net_issue(NetStream &ws, int op, float *dst) {
     if (op == 0 || !ws.dma) return;
-    const int ninst = op >> 3;
+    const int ninst = op * kNetChunk / 256;
     for (int k = ws.wave; k < ninst; k += kNetFwdWaves)
         __builtin_amdgcn_global_load_lds(
             (__attribute__((address_space(1))) void *)(ws.next + k * 256 + ws.lane * 4),
@@ -260,33 +262,36 @@ __device__ __forceinline__ void net_layer0(NetStream &ws, int nch, int op_next, 
     // what position q of the padded sequence loads: a real chunk, the padding
     // (nothing), or the next layer's first chunk
     auto op_at = [&](int q) { return q < nch ? op : (q == nch && (nch & 1) ? 0 : op_next); };
-    net_f4 xn[2];
+    constexpr int H = kNetHalves;
+    net_f4 xn[H], xc[H];
     auto xload = [&](int lc) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t) xn[t] = 2 * lc + t < F16 ? xf(2 * lc + t) : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int t = 0; t < H; ++t) xn[t] = H * lc + t < F16 ? xf(H * lc + t) : net_f4{0.0f, 0.0f, 0.0f, 0.0f};
     };
     xload(0);
     // the X operands are copied out before the next DMA issues (vmcnt counts
-    // in order: a later use would wait for that DMA as well)
+    // in order: a later use would wait for that DMA as well).  A 16-row block
+    // past the features (F = 784 fills 24.5 32-row chunks) is zero rows times
+    // zero features: skipped.
     for (int lc = 0; lc < nch; lc += 2) {
         net_chunk_wait();
-        net_f4 x0 = xn[0], x1 = xn[1];
+#pragma unroll
+        for (int t = 0; t < H; ++t) xc[t] = xn[t];
         net_issue(ws, op_at(lc + 1), sb);
         if (lc + 1 < nch) xload(lc + 1);
-        // (a chunk half past the features -- F = 784 fills 24.5 chunks -- is
-        // zero rows times zero features: skipped)
-        if (active) {
-            net_half_mm<NCG, true>(sa, 0, g, n, x0, hout);
-            if (2 * lc + 1 < F16) net_half_mm<NCG, true>(sa, 1, g, n, x1, hout);
-        }
+        if (active)
+#pragma unroll
+            for (int t = 0; t < H; ++t)
+                if (t == 0 || H * lc + t < F16) net_half_mm<NCG, true>(sa, t, g, n, xc[t], hout);
         net_chunk_wait();
-        x0 = xn[0];
-        x1 = xn[1];
+#pragma unroll
+        for (int t = 0; t < H; ++t) xc[t] = xn[t];
         net_issue(ws, op_at(lc + 2), sa);
         if (lc + 1 < nch && active) {                       // not the padding chunk
             if (lc + 2 < nch) xload(lc + 2);
-            net_half_mm<NCG, true>(sb, 0, g, n, x0, hout);
-            if (2 * lc + 3 < F16) net_half_mm<NCG, true>(sb, 1, g, n, x1, hout);
+#pragma unroll
+            for (int t = 0; t < H; ++t)
+                if (t == 0 || H * (lc + 1) + t < F16) net_half_mm<NCG, true>(sb, t, g, n, xc[t], hout);
         }
     }
 }
@@ -300,22 +305,20 @@ template <int NCG>
 __device__ __forceinline__ void net_layer(NetStream &ws, int nch, int op_next, int g, int n,
                                           float *sa, float *sb, bool active, net_f4 (&hin)[16],
                                           net_f4 (&hout)[16]) {
-    constexpr int op = 64 * NCG;
+    constexpr int op = 64 * NCG, H = kNetHalves;
     for (int lc = 0; lc < nch; lc += 2) {
         net_chunk_wait();
         net_issue(ws, op, sb);                              // lc + 1 < nch: nch is even
-        if (active) {
-            net_half_mm<NCG, false>(sa, 0, g, n, hin[0], hout);
-            net_half_mm<NCG, false>(sa, 1, g, n, hin[1], hout);
-        }
+        if (active)
+#pragma unroll
+            for (int t = 0; t < H; ++t) net_half_mm<NCG, false>(sa, t, g, n, hin[t], hout);
         net_chunk_wait();
         net_issue(ws, lc + 2 < nch ? op : op_next, sa);
-        if (active) {
-            net_half_mm<NCG, false>(sb, 0, g, n, hin[2], hout);
-            net_half_mm<NCG, false>(sb, 1, g, n, hin[3], hout);
-        }
+        if (active)
 #pragma unroll
-        for (int i = 0; i < 12; ++i) hin[i] = hin[i + 4];
+            for (int t = 0; t < H; ++t) net_half_mm<NCG, false>(sb, t, g, n, hin[H + t], hout);
+#pragma unroll
+        for (int i = 0; i < 16 - 2 * H; ++i) hin[i] = hin[i + 2 * H];
     }
 }
 
@@ -335,21 +338,20 @@ __device__ __forceinline__ void net_half_mm_narrow(const float *sl, int s, int g
 
 __device__ __forceinline__ void net_layer_narrow(NetStream &ws, int nch, int g, int n, float *sa, float *sb,
                                                  bool active, net_f4 (&hin)[16], net_f4 &h0) {
+    constexpr int H = kNetHalves;
     for (int lc = 0; lc < nch; lc += 2) {
         net_chunk_wait();
         net_issue(ws, 64, sb);                              // lc + 1 < nch: nch is even
-        if (active) {
-            net_half_mm_narrow(sa, 0, g, n, hin[0], h0);
-            net_half_mm_narrow(sa, 1, g, n, hin[1], h0);
-        }
+        if (active)
+#pragma unroll
+            for (int t = 0; t < H; ++t) net_half_mm_narrow(sa, t, g, n, hin[t], h0);
         net_chunk_wait();
         if (lc + 2 < nch) net_issue(ws, 64, sa);
-        if (active) {
-            net_half_mm_narrow(sb, 0, g, n, hin[2], h0);
-            net_half_mm_narrow(sb, 1, g, n, hin[3], h0);
-        }
+        if (active)
 #pragma unroll
-        for (int i = 0; i < 12; ++i) hin[i] = hin[i + 4];
+            for (int t = 0; t < H; ++t) net_half_mm_narrow(sb, t, g, n, hin[H + t], h0);
+#pragma unroll
+        for (int i = 0; i < 16 - 2 * H; ++i) hin[i] = hin[i + 2 * H];
     }
 }
 
@@ -388,7 +390,8 @@ __device__ __forceinline__ void net_producer(const NetFwdArgs &a, int e, int pw,
         *reinterpret_cast<net_f4 *>(sbias + s4) = w;
     }
     const int nch0 = a.g.nchunk[0], p0 = nch0 + (nch0 & 1);
-    const int np = p0 + (nl - 1) * 2 * NCGH;
+    constexpr int PL = OPH / kNetChunk;                     // chunk positions of layers >= 1
+    const int np = p0 + (nl - 1) * PL;
     net_f4 wv[R];
     float av[R][4];
     // chunk position p -> layer, chunk (false: layer 0's padding or the end)
@@ -398,8 +401,8 @@ __device__ __forceinline__ void net_producer(const NetFwdArgs &a, int e, int pw,
             c = p;
             return p < nch0;
         }
-        l = 1 + (p - p0) / (2 * NCGH);
-        c = (p - p0) % (2 * NCGH);
+        l = 1 + (p - p0) / PL;
+        c = (p - p0) % PL;
         return p < np;
     };
     auto load = [&](int p) {
@@ -464,7 +467,7 @@ __device__ __forceinline__ void net_producer(const NetFwdArgs &a, int e, int pw,
 // dataset rows read straight from X through the env's row order -- replaces
 // net_update_kernel, net_gather_kernel and the separate minibatch forward.
 template <int NCGH, bool NARROW, bool FUSED>
-__global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
+__global__ __launch_bounds__(kNetThreads, kNetFwdOcc) void net_fwd_kernel(NetFwdArgs a) {
     constexpr int OPH = 64 * NCGH;
     __shared__ __attribute__((aligned(16))) float slot_a[kNetSlotFloats];
     __shared__ __attribute__((aligned(16))) float slot_b[kNetSlotFloats];
@@ -565,7 +568,7 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
         }
         if (l + 2 < nl) {
             bias_init(l + 1, NCGH);
-            net_layer<NCGH>(ws, 2 * NCGH, op_of(l + 2), g, n, slot_a, slot_b, active, hin, hout);
+            net_layer<NCGH>(ws, OPH / kNetChunk, op_of(l + 2), g, n, slot_a, slot_b, active, hin, hout);
         }
     }
     const int K = a.g.dout[nl - 1];
@@ -574,7 +577,7 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
         // bias of unit 4 g + i: permuted slot 16 i + g of the layer (net_bias_slot)
 #pragma unroll
         for (int i = 0; i < 4; ++i) hout[0][i] = sbias[(nl - 1) * OPH + 16 * i + g];
-        net_layer_narrow(ws, 2 * NCGH, g, n, slot_a, slot_b, active, hin, hout[0]);
+        net_layer_narrow(ws, OPH / kNetChunk, g, n, slot_a, slot_b, active, hin, hout[0]);
         // class 4 g' + i of row n sits in lane 16 g' + n, register i
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -584,7 +587,7 @@ __global__ __launch_bounds__(kNetThreads, 2) void net_fwd_kernel(NetFwdArgs a) {
         for (int k = 16; k < kNetMaxClasses; ++k) z[k] = 0.0f;
     } else {
         bias_init(nl - 1, 1);
-        net_layer<1>(ws, 2 * NCGH, 0, g, n, slot_a, slot_b, active, hin, hout);   // the output layer
+        net_layer<1>(ws, OPH / kNetChunk, 0, g, n, slot_a, slot_b, active, hin, hout);   // the output layer
         // class 16g + 4i + j of row n sits in lane group g: lane group 0
         // gathers the row
 #pragma unroll
