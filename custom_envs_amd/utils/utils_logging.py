@@ -124,10 +124,14 @@ class VecMonitor:
     """
 
     def __init__(self, num_envs, file_paths=None, info_keywords=(), chunk_size=1,
-                 callbacks=None, style='logging', allow_early_resets=True):
+                 callbacks=None, style='logging', allow_early_resets=True,
+                 reset_keywords=()):
         if style not in ('logging', 'sb'):
             raise ValueError('style must be logging or sb')
         self.style = style
+        self.reset_keywords = tuple(reset_keywords or ())
+        if self.reset_keywords and style != 'sb':
+            raise ValueError('reset_keywords belong to the sb style')
         self.allow_early_resets = bool(allow_early_resets)
         self.needs_reset = np.ones(num_envs, bool)
         self.num_envs = num_envs
@@ -145,17 +149,28 @@ class VecMonitor:
         self.data = [[] for _ in range(num_envs)]
         self.metric_history = [defaultdict(list) for _ in range(num_envs)]
         self.total_steps = np.zeros(num_envs, np.int64)
+        self.reset_info = {}
 
-    def reset(self, indices=None):
+    def reset(self, indices=None, **kwargs):
         idx = slice(None) if indices is None else indices
         if self.style == 'sb' and not self.allow_early_resets and not self.needs_reset[idx].all():
             raise RuntimeError('Tried to reset an environment before done. If you want to '
                                'allow early resets, wrap your env with Monitor(env, path, '
                                'allow_early_resets=True)')
-        self.needs_reset[idx] = False
+        self.needs_reset[idx] = False         # before the keyword check, monitor.py:84-85
+        for key in self.reset_keywords:
+            if kwargs.get(key) is None:
+                raise ValueError('Expected you to pass kwarg %s into reset' % key)
+            self.reset_info[key] = kwargs[key]
         self.ep_reward[idx] = 0.0
         self.ep_len[idx] = 0
         self.current_episode[idx] += 1
+
+    def check_step(self):
+        """Called before the engine launches a step: the SB Monitor refuses
+        to step an env that needs a reset (monitor.py:87-88)."""
+        if self.style == 'sb' and self.needs_reset.any():
+            raise RuntimeError('Tried to step environment that needs reset')
 
     def step(self, rewards, dones, infos, observations=None):
         rewards = np.asarray(rewards, dtype=np.float64)
@@ -182,6 +197,7 @@ class VecMonitor:
                 ep_info['episode'] = int(self.current_episode[i])
             for key in self.info_keywords:
                 ep_info[key] = info[key]
+            ep_info.update(self.reset_info)
             self.data[i].append(ep_info)
             if len(self.data[i]) >= self.chunk_size:
                 _save_rows(self.paths[i], self.data[i])

@@ -43,9 +43,9 @@ def monitor_parts(fn):
         current_reward, episode + info_keywords;
       - the stable-baselines style custom_envs.wrappers.Monitor
         (wrappers/monitor.py:11-163): rows r, l, t + info_keywords, the
-        reset-before-done check (``allow_early_resets``).  Its
-        ``reset_keywords`` need kwargs a VecEnv reset never passes, so a
-        factory that sets them is not batched (target None).
+        reset-before-done check (``allow_early_resets``) and the
+        ``reset_keywords`` check (a VecEnv reset passes no kwargs, so the
+        batched reset raises the per-env Monitor's ValueError).
     ``VecMonitor`` writes the same ``.mon.csv`` rows in either style."""
     from custom_envs_amd.utils.utils_logging import Monitor
     from custom_envs_amd.wrappers.monitor import Monitor as SBMonitor
@@ -56,8 +56,7 @@ def monitor_parts(fn):
     kw = dict(fn.keywords)
     path = fn.args[1] if len(fn.args) > 1 else kw.pop('file_path', None)
     if fn.func is SBMonitor:
-        if tuple(kw.pop('reset_keywords', ()) or ()):
-            return None, None
+        kw['reset_keywords'] = tuple(kw.get('reset_keywords', ()) or ())
         kw['style'] = 'sb'
         kw['allow_early_resets'] = bool(kw.get('allow_early_resets', False))
     else:

@@ -80,7 +80,8 @@ class GPUVecEnv:
                                       chunk_size=mkw.get('chunk_size', 1),
                                       callbacks=mkw.get('callbacks'),
                                       style=mkw.get('style', 'logging'),
-                                      allow_early_resets=mkw.get('allow_early_resets', True))
+                                      allow_early_resets=mkw.get('allow_early_resets', True),
+                                      reset_keywords=mkw.get('reset_keywords', ()))
         self.current_step = np.zeros(self.num_envs, np.int64)
         self.waiting = False
         self.closed = False
@@ -109,6 +110,8 @@ class GPUVecEnv:
         return self.engine.reset()
 
     def step_async(self, actions):
+        if self.monitor is not None:
+            self.monitor.check_step()
         self.engine.step_async(actions)
         self.waiting = True
 

@@ -165,7 +165,8 @@ class OptVecEnv:
                                           chunk_size=mkw.get('chunk_size', 1),
                                           callbacks=mkw.get('callbacks'),
                                           style=mkw.get('style', 'logging'),
-                                          allow_early_resets=mkw.get('allow_early_resets', True))
+                                          allow_early_resets=mkw.get('allow_early_resets', True),
+                                          reset_keywords=mkw.get('reset_keywords', ()))
         else:
             runners = [functools.partial(OptEnvRunner, fn) for fn in environment_fns]
             self._host = ThreadVecEnv(runners)
@@ -179,6 +180,8 @@ class OptVecEnv:
         return self._engine is not None
 
     def step_async(self, actions):
+        if self._engine is not None and self.monitor is not None:
+            self.monitor.check_step()
         self.waiting = True
         if self._engine is not None:
             self._engine.step_async(np.asarray(actions, np.float32).reshape(-1))

@@ -173,3 +173,22 @@ def test_sb_monitor_refuses_early_reset(lr_dataset):
     with pytest.raises(RuntimeError, match='allow early resets'):
         venv.reset()
     venv.close()
+
+
+def test_sb_monitor_reset_keywords_batch_and_raise(lr_dataset):
+    """An SB Monitor factory with ``reset_keywords`` batches into one engine;
+    its VecEnv reset (which passes no kwargs) raises the per-env wrapper's
+    ValueError (monitor.py:76-80), and a step before any reset raises its
+    RuntimeError (monitor.py:87-88), before the engine launches."""
+    import custom_envs
+    from custom_envs.vectorize import ThreadVecEnv
+    from custom_envs.wrappers import Monitor
+    fns = [functools.partial(Monitor, custom_envs.make('Optimize-v0', data_set=lr_dataset), None,
+                             reset_keywords=('tag',)) for _ in range(3)]
+    venv = ThreadVecEnv(fns)
+    assert venv.engine_backed
+    with pytest.raises(RuntimeError, match='needs reset'):
+        venv.step(np.zeros((3, 20), np.float32))
+    with pytest.raises(ValueError, match='kwarg tag'):
+        venv.reset()
+    venv.close()

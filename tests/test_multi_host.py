@@ -224,6 +224,32 @@ def test_sb_monitor_contract(tmp_path):
     env.close()
 
 
+def test_vec_monitor_sb_reset_keywords_and_step_check(tmp_path):
+    """The batched SB Monitor: step before reset and a reset without the
+    reset_keywords raise as the per-env wrapper does (monitor.py:76-88); the
+    keyword values ride on every episode row."""
+    from custom_envs_amd.utils.utils_logging import VecMonitor
+    mon = VecMonitor(2, str(tmp_path / 'v'), style='sb', reset_keywords=('tag',))
+    with pytest.raises(RuntimeError, match='needs reset'):
+        mon.check_step()
+    with pytest.raises(ValueError, match='kwarg tag'):
+        mon.reset()
+    mon.check_step()             # the episode counted as started (monitor.py:84-85)
+    mon = VecMonitor(2, str(tmp_path / 'w'), style='sb', allow_early_resets=True,
+                     reset_keywords=('tag',))
+    mon.reset(tag='x')
+    assert mon.step(np.array([1.0, 2.0]), np.array([False, False]), [{}, {}]) == {}
+    # the auto-reset after an episode passes no kwargs: it raises as the
+    # worker's ``env.reset()`` would (utils_venv.py:31), after the row is kept
+    with pytest.raises(ValueError, match='kwarg tag'):
+        mon.step(np.array([1.0, 2.0]), np.array([True, False]), [{}, {}])
+    import pandas as pd
+    row = pd.read_csv(tmp_path / 'w_0.mon.csv').iloc[0]
+    assert (row['r'], row['l'], row['tag']) == (2.0, 2, 'x')
+    with pytest.raises(ValueError):
+        VecMonitor(1, None, reset_keywords=('tag',))
+
+
 def test_history_and_subset_wrappers():
     from custom_envs_amd.wrappers import HistoryWrapper, SubSetWrapper
     env = HistoryWrapper(StubMultiEnv(2), max_history=3)
