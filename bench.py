@@ -964,7 +964,7 @@ def nn_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
             'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
             'kernel': 'one step = ce::nn_grad_kernel, nn_update_kernel, nn_step_kernel, '
-                      'nn_agent_kernel (dominant), nn_finalize_kernel',
+                      'nn_agent_rows_kernel (dominant), nn_finalize_kernel',
             'bytes_per_env_step': bpe,
             'step_ms_median': kernel_ms, 'step_ms_mean': kernel_ms_mean,
             'flops_per_env_step': flops,
