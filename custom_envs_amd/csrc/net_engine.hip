@@ -162,6 +162,13 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
         net_destroy(p);
         return code;
     };
+    // a HIP failure after the plan exists frees it (CE_HIP would return past it)
+#define NET_HIP(call)                                                                     \
+    do {                                                                                  \
+        const hipError_t err_ = (call);                                                   \
+        if (err_ != hipSuccess)                                                           \
+            return bail(fail(CE_EHIP, std::string(#call " failed: ") + hipGetErrorString(err_))); \
+    } while (0)
     p->g = geo;
     p->E = a.E;
     p->N = a.N;
@@ -176,7 +183,7 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
         const size_t nrb = static_cast<size_t>(p->T) * (kNetTile / 16);
         std::vector<float> xt(nrb * p->F16 * 64 * 4, 0.0f);
         std::vector<float> xh(N * a.F);
-        CE_HIP(hipMemcpy(xh.data(), a.X, xh.size() * sizeof(float), hipMemcpyDeviceToHost));
+        NET_HIP(hipMemcpy(xh.data(), a.X, xh.size() * sizeof(float), hipMemcpyDeviceToHost));
         for (size_t rb = 0; rb < nrb; ++rb)
             for (int t = 0; t < p->F16; ++t)
                 for (int ln = 0; ln < 64; ++ln)
@@ -187,7 +194,7 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
                             xt[((rb * p->F16 + t) * 64 + ln) * 4 + q] = xh[r * a.F + f];
                     }
         if ((rc = dev_alloc(&p->Xt, xt.size())) != CE_OK) return bail(rc);
-        CE_HIP(hipMemcpy(p->Xt, xt.data(), xt.size() * sizeof(float), hipMemcpyHostToDevice));
+        NET_HIP(hipMemcpy(p->Xt, xt.data(), xt.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     if (B < N) {
         p->Tmb = (a.B + kNetTile - 1) / kNetTile;
@@ -227,7 +234,8 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
     // workgroups at 1024 envs, dispatch-bound (0.99 ms for 3.3 GB)
     const int rows = geo.row0[nl] + (geo.bias_total + 255) / 256;
     p->upd_blocks = std::max(1, std::min(kNetUpdBlocks, (rows + 15) / 16));
-    CE_HIP(hipDeviceSynchronize());
+    NET_HIP(hipDeviceSynchronize());
+#undef NET_HIP
     *out = p;
     return CE_OK;
 }
