@@ -82,11 +82,11 @@ bool complete(const ce_multi_outputs *o) {
 // one step's five launches; the ping-pong pairs swap afterwards
 void launch_step(ce_nn_engine *e, const float *act, const ce_multi_outputs &o, hipStream_t s) {
     const ce::NnArgs a = make_args(e, act, o);
-    const size_t stage = (static_cast<size_t>(ce::kNnChunk) * 3 * a.H + 4) * sizeof(float);
+    const size_t stage = (static_cast<size_t>(ce::kNnRows) * 3 * a.H + 4) * sizeof(float);
     hipLaunchKernelGGL(ce::nn_grad_kernel, dim3(a.E), dim3(ce::kNnBlock), a.lds_bytes, s, a);
     hipLaunchKernelGGL(ce::nn_update_kernel, dim3(a.nchunk_u, a.E), dim3(ce::kNnChunk), 0, s, a);
     hipLaunchKernelGGL(ce::nn_step_kernel, dim3(a.E), dim3(ce::kNnBlock), a.lds_bytes, s, a);
-    hipLaunchKernelGGL(ce::nn_agent_rows_kernel, dim3(a.nchunk, a.E), dim3(ce::kNnChunk), stage, s, a);
+    hipLaunchKernelGGL(ce::nn_agent_rows_kernel, dim3(a.nchunk, a.E), dim3(ce::kNnRows), stage, s, a);
     hipLaunchKernelGGL(ce::nn_finalize_kernel, dim3(a.E), dim3(ce::kNnChunk), 0, s, a);
     e->parity ^= 1;
 }
@@ -195,7 +195,7 @@ int ce_nn_create(const ce_nn_config *cfg, const float *features, const int32_t *
     e->P = a.P = static_cast<int>(P);
     e->Ps = static_cast<size_t>((P + 63) & ~63L);
     a.Ps = static_cast<int>(e->Ps);
-    a.nchunk = static_cast<int>((P + ce::kNnChunk - 1) / ce::kNnChunk);
+    a.nchunk = static_cast<int>((P + ce::kNnRows - 1) / ce::kNnRows);
     a.nchunk_u = static_cast<int>((P + ce::kNnChunk * ce::kNnUpdPer - 1) /
                                   (ce::kNnChunk * ce::kNnUpdPer));
     // LDS: X, every hidden activation, the logits, the split-k scratch

@@ -63,7 +63,11 @@ constexpr int kNnMaxWidth = 512;   // hidden units per layer (multiple of 32)
 constexpr int kNnMaxK = 32;        // classes
 constexpr int kNnMaxH = 16;        // adjusted-history length
 constexpr int kNnPad = 4;          // LDS row padding (floats)
-constexpr int kNnChunk = 256;      // threads (and observation rows) per block of nn_agent_rows_kernel
+constexpr int kNnChunk = 256;      // threads per block of the update / finalize kernels
+#ifndef CE_NN_ROWS
+#define CE_NN_ROWS 256
+#endif
+constexpr int kNnRows = CE_NN_ROWS;  // threads (and observation rows) per block of nn_agent_rows_kernel
 constexpr int kNnUpdPer = 4;       // agents per thread of nn_update_kernel
 constexpr int kNnPrefetch = 8;     // 8-float k-chunks of W in flight per lane
 
@@ -90,7 +94,7 @@ struct NnArgs {
     float *loss_b;                 // [E] minibatch loss at theta'
     double *part_u;                // [E][nchunk_u][3] update sums (lr, lr^2, reset gradient)
     double *part_c;                // [E][nchunk][5] agent sums (|theta'|, |w~|, |g~|, g, |dg|)
-    int nchunk;                    // nn_agent_rows_kernel blocks per env (kNnChunk rows each)
+    int nchunk;                    // nn_agent_rows_kernel blocks per env (kNnRows rows each)
     int nchunk_u;                  // nn_update_kernel blocks per env
     float *rw, *rg;                // [H][E][Ps] adjusted w~ / g~ entries, obs form
     double *al;                    // [H][E] adjusted loss entries (raw)
@@ -689,15 +693,15 @@ __device__ __forceinline__ NnStepScalars nn_step_scalars(const NnArgs &a, size_t
 //     row_agent, which in sorted-name order is runs of consecutive agents.
 //   - The per-block sums (|theta'|, |w~|, |g~|, g, |dg|) are sums over the
 //     same agents in another order.
-__global__ __launch_bounds__(kNnChunk) void nn_agent_rows_kernel(NnArgs a) {
+__global__ __launch_bounds__(kNnRows) void nn_agent_rows_kernel(NnArgs a) {
 #pragma clang fp contract(off)
-    extern __shared__ float4 stage4[];             // [kNnChunk * 3H + 4] rows at the run's phase
+    extern __shared__ float4 stage4[];             // [kNnRows * 3H + 4] rows at the run's phase
     float *stage = reinterpret_cast<float *>(stage4);
     __shared__ float lobs[kNnMaxH];
-    __shared__ double red[(kNnChunk / 64) * 5];
+    __shared__ double red[(kNnRows / 64) * 5];
     const size_t e = blockIdx.y, ps = a.Ps, E = a.E;
     const int chunk = blockIdx.x, tid = threadIdx.x, H = a.H, W = 3 * H;
-    const int r0 = chunk * kNnChunk;
+    const int r0 = chunk * kNnRows;
     const int r = r0 + tid;
     const bool on = r < a.P;
     const int rc = on ? r : r0;
@@ -762,7 +766,7 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_rows_kernel(NnArgs a) {
         }
     }
     __syncthreads();
-    const int n = (a.P - r0 < kNnChunk ? a.P - r0 : kNnChunk) * W;
+    const int n = (a.P - r0 < kNnRows ? a.P - r0 : kNnRows) * W;
     const size_t a0 = g0 + ((4 - off) & 3);             // first 16-byte-aligned float
     const size_t a1 = a0 + ((g0 + n - a0) & ~size_t(3)) * (g0 + n >= a0);   // end of whole units
     float *obs = a.obs;
@@ -777,12 +781,12 @@ __global__ __launch_bounds__(kNnChunk) void nn_agent_rows_kernel(NnArgs a) {
             const int nb = static_cast<int>((a1 - a0) >> 2);
             const float4 *src = reinterpret_cast<const float4 *>(stage + off + head);
             float4 *dst = reinterpret_cast<float4 *>(obs + a0);
-            for (int i = tid; i < nb; i += kNnChunk) dst[i] = src[i];
+            for (int i = tid; i < nb; i += kNnRows) dst[i] = src[i];
         } else {
-            for (int i = tid; i < n; i += kNnChunk) obs[g0 + i] = stage[off + i];
+            for (int i = tid; i < n; i += kNnRows) obs[g0 + i] = stage[off + i];
         }
     }
-    nn_block_sum<5, kNnChunk>(v, red);
+    nn_block_sum<5, kNnRows>(v, red);
     if (tid == 0) {
         double *o = a.part_c + (e * a.nchunk + chunk) * 5;
         for (int k = 0; k < 5; ++k) o[k] = v[k];
