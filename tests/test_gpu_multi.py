@@ -171,6 +171,48 @@ def test_config5_benchmark_size_sampled_envs():
         eng.close()
 
 
+def test_long_run_many_episodes_against_oracle():
+    """600 steps with max_batches = 45 (13 episodes, auto-resets and loss >
+    1e4 early stops mixed): the rings, step counters and row order across
+    many episodes, six sampled envs of 256 against live oracle runners at
+    every step (multioptlrs.py:80-129, optvecenv.py:37-48)."""
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    E, P, H, MB, T = 256, 4, 5, 45, 600
+    sample = [0, 1, 63, 64, 254, 255]
+    rs = np.random.RandomState(23)
+    lows = rs.uniform(-1.0, 2.0, E)
+    actions = np.stack([rs.uniform(lows[e], lows[e] + 1.0, (T, P)) for e in range(E)], 1)
+    actions = actions.astype(np.float32)                       # [T][E][P]
+    eng = MultiOptEngine(E, 'func4', max_batches=MB, max_history=H)
+    refs = [OptEnvRunner(OracleMulti(P, max_batches=MB, max_history=H)) for _ in sample]
+    try:
+        first = eng.reset()
+        for e, r in zip(sample, refs):
+            assert np.array_equal(first[e * P:(e + 1) * P], np.stack(r.reset()))
+        episodes = 0
+        for t in range(T):
+            out = eng.step(actions[t])
+            eng_theta = eng.get_state()['theta']
+            for e, runner in zip(sample, refs):
+                states, rewards, dones, infos = runner.step(list(actions[t, e].reshape(P, 1)))
+                grad_abs = np.abs(runner._environment.history['gradients']).astype(np.float64)
+                if dones[0]:
+                    episodes += 1
+                    states = runner.reset()
+                rows = slice(e * P, (e + 1) * P)
+                what = (t, e)
+                assert np.all(out['done'][rows] == dones[0]), what
+                assert int(out['episode_len'][e]) == infos[0]['episode']['l'], what
+                _close_rows(out['obs'][rows], np.stack(states))
+                assert abs(out['reward'][e * P] - rewards[0]) <= 1e-6 * max(1.0, abs(rewards[0])), what
+                if not dones[0]:
+                    assert np.array_equal(eng_theta[e], runner._environment.model.params), what
+                _close_info(out['info'][e], _ref_info(infos[0]), grad_abs=grad_abs)
+        assert episodes >= 6 * 10
+    finally:
+        eng.close()
+
+
 def test_single_env_api_matches_oracle():
     from custom_envs_amd import make
     env = make('MultiOptLRs-v0', problem='func', max_batches=12)

@@ -309,3 +309,57 @@ def test_benchmark_config_against_live_oracle(lr_dataset):
         np.testing.assert_allclose(st['weights'][i], env.model.weights.ravel(), rtol=1e-12,
                                    atol=1e-14)
     eng.close()
+
+
+def test_long_run_device_path_against_oracle(lr_dataset):
+    """1000 steps (25 episodes, 24 in-kernel auto-resets) of the benchmark
+    kernel through the bench's own device path -- chunks of 20 plain launches
+    and of 50 as a replayed hipGraph -- against live oracle envs: at every
+    chunk end the last step's outputs, and at the end the float64 weights and
+    loss history, so no drift across episodes goes unseen
+    (optimize.py:69-100, utils_venv.py:31)."""
+    import torch
+    E, P, T = 512, 20, 1000
+    check = [0, 1, 15, 16, 255, 256, 510, 511]
+    eng = _engine(lr_dataset, E)
+    assert eng.step_kernel == 'optimize_lr_mfma_kernel<3,3,4>'
+    eng.seed(list(range(E)))
+    refs = {}
+    for i in check:
+        env = OracleEnv(*lr_dataset)
+        env.seed(i)
+        env.reset()
+        refs[i] = env
+    rs = np.random.RandomState(77)
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        eng.set_stream(stream.cuda_stream)
+        out = eng.alloc_device_outputs()
+        eng.reset_device(out)
+        t = 0
+        while t < T:
+            k = min(20 if (t // 70) % 2 == 0 else 50, T - t)
+            acts = rs.normal(0, 0.01, (k, E, P)).astype(np.float32)
+            eng.step_many_device(k, torch.from_numpy(acts).cuda(), out)
+            stream.synchronize()
+            got = {name: out[name].cpu().numpy() for name in ('obs', 'reward', 'done', 'episode_len',
+                                                               'objective', 'accuracy')}
+            for i, env in refs.items():
+                for s in range(k):
+                    obs, rew, done, info = env.step(acts[s, i])
+                    if done:
+                        obs = env.reset()
+                assert bool(got['done'][i]) == done, (i, t + k)
+                assert got['episode_len'][i] == info['episode']['l'], (i, t + k)
+                np.testing.assert_allclose(got['obs'][i], obs, rtol=F64_RTOL, atol=F64_ATOL,
+                                           err_msg='env %d step %d' % (i, t + k))
+                assert got['reward'][i] == pytest.approx(rew, rel=F64_RTOL), (i, t + k)
+                assert got['objective'][i] == pytest.approx(info['objective'], rel=F64_RTOL)
+                assert got['accuracy'][i] == np.float32(info['accuracy']), (i, t + k)
+            t += k
+    st = eng.get_state()
+    for i, env in refs.items():
+        np.testing.assert_allclose(st['weights'][i], env.model.weights.ravel(), rtol=1e-12,
+                                   atol=1e-14)
+        assert st['step'][i] == T % 40
+    eng.close()
