@@ -243,6 +243,20 @@ def test_small_networks_against_oracle(hidden):
         _check_env(ds, hidden, seed, acts[:, i * P:(i + 1) * P], rows, rec, i, 7)
 
 
+def test_long_run_small_network_against_oracle():
+    """64 steps with max_batches 11: five auto-resets and a dozen epoch ends
+    (each a reshuffle composed into the row order), the rings wrapping many
+    times, three envs against live oracle envs."""
+    ds = _iris()
+    seeds = [2, 31, 77]
+    hidden = (32,)
+    P = 4 * 32 + 32 + 32 * 3 + 3
+    acts = _actions(64, len(seeds), P, 1.0, 2.5, 12)
+    _, rows, rec = _run_engine(ds, hidden, seeds, acts, max_batches=11)
+    for i, seed in enumerate(seeds):
+        _check_env(ds, hidden, seed, acts[:, i * P:(i + 1) * P], rows, rec, i, 11)
+
+
 def test_many_classes_against_oracle():
     """7 classes (past the eval kernels' compiled 4-class instance, nn_km):
     the 32-class-bound instance of nn_grad_kernel / nn_step_kernel, with a
