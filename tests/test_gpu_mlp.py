@@ -122,6 +122,52 @@ def test_config3_envs_against_live_oracle():
         eng.close()
 
 
+def test_config3_long_run_against_oracle():
+    """205 steps of the fused config-3 kernel (five auto-resets): each reset
+    composes the env's minibatch row order with its reset shuffle, so after
+    five episodes every B = 32 minibatch still has to be the oracle's
+    InMemoryDataSet rows (optimize.py:69-100, dataset/__init__.py); three
+    envs against live oracle envs at every step."""
+    from custom_envs_amd.data import load_data
+    seq = load_data('mnist_synthetic', batch_size=32)
+    seeds = [9, 10, 4000]
+    eng = _engine(seq.features, seq.targets, len(seeds))
+    refs = []
+    for s in seeds:
+        env = OracleEnv(seq.features, seq.targets, batch_size=32, model='mlp')
+        env.seed(s)
+        env.reset()
+        refs.append(env)
+    try:
+        assert eng.step_kernel == 'mlp_step_kernel'
+        eng.seed(seeds)
+        eng.reset()
+        P = eng.act_dim
+        rs = np.random.RandomState(31)
+        resets = 0
+        for t in range(205):
+            acts = rs.normal(0, 1e-3, (len(seeds), P)).astype(np.float32)
+            out = eng.step(acts)
+            for i, env in enumerate(refs):
+                obs, reward, done, info = env.step(acts[i])
+                if done:
+                    obs = env.reset()
+                    resets += 1
+                what = 'env %d step %d' % (seeds[i], t)
+                assert bool(out['done'][i]) == done, what
+                assert int(out['episode_len'][i]) == info['episode']['l'], what
+                _row_close(out['obs'][i], obs, what=what)
+                assert _rel(out['reward'][i], reward) <= RTOL, what
+                assert _rel(out['objective'][i], info['objective']) <= RTOL, what
+                assert out['accuracy'][i] == np.float32(info['accuracy']), what
+        assert resets == 3 * 5
+        order = eng.get_state()['order']
+        for i, env in enumerate(refs):
+            assert np.array_equal(order[i], env.sequence.order), seeds[i]
+    finally:
+        eng.close()
+
+
 def test_config3_benchmark_size_sampled_envs():
     """Config 3 at the size the bench runs it (BASELINE configs[2]: 4096
     envs, 784 -> 64 -> 10, N = 1024, B = 32): envs 0, 1, 2047, 2048, 4094 and
