@@ -1,0 +1,75 @@
+"""One rank of the world-N rehearsal on ONE GPU
+(tests/test_gpu_distributed.py::test_world_n_on_one_gpu_matches_world_1): the
+product's ShardedEnvs over a real HIP engine shard on cuda:0, the per-step
+all-gather of the packed (compact) record as a real collective between the
+rank processes (gloo: RCCL does not put two ranks on one device), serial or
+pipelined over two buffers as bench.py runs it.  Rank 0 writes the gathered
+global arrays of every step to OUT.
+
+    RANK=r WORLD_SIZE=n MASTER_ADDR=127.0.0.1 MASTER_PORT=p \\
+        python tests/gpu_dist_worker.py OUT COMPACT(0|1) PIPELINED(0|1)
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+E, STEPS, BASE = 37, 44, 500
+
+
+def main():
+    out_path, compact, pipelined = sys.argv[1], sys.argv[2] == '1', sys.argv[3] == '1'
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    import torch
+    import torch.distributed as dist
+    from custom_envs_amd.distributed import ShardedEnvs, shard_range
+    from custom_envs_amd.engine import OptimizeEngine
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    d = np.load(os.path.join(HERE, 'golden', 'lr_256x10.npz'))
+    lo, hi = shard_range(E, world, rank)
+    eng = OptimizeEngine(d['features'], d['targets'], num_envs=hi - lo)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    eng.set_stream(stream.cuda_stream)
+    shard = ShardedEnvs(eng, E, rank, world, slots=2, collective=True, compact=compact)
+    assert (shard.lo, shard.hi) == (lo, hi)
+    shard.seed(BASE)
+    shard.reset(0)
+    acts = np.random.RandomState(8).normal(0, 0.02, (STEPS, E, 20)).astype(np.float32)
+    dacts = torch.from_numpy(np.ascontiguousarray(acts[:, lo:hi])).cuda()
+    keys = ('obs', 'done', 'episode_len', 'reward', 'objective', 'accuracy')
+    got, pending = {}, [None, None]
+
+    def collect(entry):
+        work, res, t = entry
+        work.wait()
+        got[t] = {k: res[k].cpu().numpy() for k in keys}
+
+    for t in range(STEPS):
+        slot = t & 1 if pipelined else 0
+        if pending[slot] is not None:
+            collect(pending[slot])
+            pending[slot] = None
+        shard.step(dacts[t], slot)
+        res, work = shard.gather(slot, async_op=True)
+        pending[slot] = (work, res, t)
+        if not pipelined:
+            collect(pending[slot])
+            pending[slot] = None
+    for slot in (0, 1):
+        if pending[slot] is not None:
+            collect(pending[slot])
+    torch.cuda.synchronize()
+    if rank == 0:
+        np.savez(out_path, **{k: np.stack([got[t][k] for t in range(STEPS)]) for k in keys})
+    eng.close()
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

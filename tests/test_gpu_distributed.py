@@ -183,3 +183,45 @@ def test_sharded_multiagent_gather_matches_oracle(nccl_world1):
     finally:
         eng.close()
         torch.cuda.set_stream(torch.cuda.default_stream())
+
+
+@pytest.mark.parametrize('world,compact,pipelined', [(2, True, False), (3, True, True),
+                                                     (2, False, True)])
+def test_world_n_on_one_gpu_matches_world_1(tmp_path, world, compact, pipelined):
+    """N > 1 data movement with real HIP engine shards: `world` rank
+    processes on this one GPU (tests/gpu_dist_worker.py), each stepping its
+    contiguous shard of 37 envs (uneven splits) and all-gathering the packed
+    record every step through the product's ShardedEnvs (gloo carries the
+    collective between processes on one device); the gathered global arrays
+    of every step must equal a 1-rank run bit for bit (seeds = global index,
+    so the sharding is invisible in the results)."""
+    import subprocess
+    import sys
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'gpu_dist_worker.py')
+
+    def run(n, out):
+        with socket.socket() as s:
+            s.bind(('127.0.0.1', 0))
+            port = s.getsockname()[1]
+        procs = []
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1',
+                       MASTER_PORT=str(port), LOCAL_RANK='0')
+            procs.append(subprocess.Popen([sys.executable, worker, str(out), str(int(compact)),
+                                           str(int(pipelined))], env=env))
+        codes = []
+        for p in procs:
+            try:
+                codes.append(p.wait(timeout=150))
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        assert codes == [0] * n, codes
+        return np.load(out)
+
+    one = run(1, tmp_path / 'w1.npz')
+    many = run(world, tmp_path / 'wn.npz')
+    for k in one.files:
+        assert np.array_equal(one[k], many[k]), k
+    assert one['obs'].shape == (44, 37, 41) and one['done'].any()
