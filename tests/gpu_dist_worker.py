@@ -7,7 +7,10 @@ pipelined over two buffers as bench.py runs it.  Rank 0 writes the gathered
 global arrays of every step to OUT.
 
     RANK=r WORLD_SIZE=n MASTER_ADDR=127.0.0.1 MASTER_PORT=p \\
-        python tests/gpu_dist_worker.py OUT COMPACT(0|1) PIPELINED(0|1)
+        python tests/gpu_dist_worker.py OUT COMPACT(0|1) PIPELINED(0|1) [multi]
+
+``multi``: config 5's MultiOptEngine (13 envs x 4 agents, func4, H = 5,
+max_batches = 30) instead of Optimize-v0.
 """
 import os
 import sys
@@ -22,6 +25,8 @@ E, STEPS, BASE = 37, 44, 500
 
 def main():
     out_path, compact, pipelined = sys.argv[1], sys.argv[2] == '1', sys.argv[3] == '1'
+    if len(sys.argv) > 4 and sys.argv[4] == 'multi':
+        return main_multi(out_path, pipelined)
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
     import torch
     import torch.distributed as dist
@@ -66,6 +71,42 @@ def main():
     torch.cuda.synchronize()
     if rank == 0:
         np.savez(out_path, **{k: np.stack([got[t][k] for t in range(STEPS)]) for k in keys})
+    eng.close()
+    dist.destroy_process_group()
+    return 0
+
+
+def main_multi(out_path, pipelined):
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    import torch
+    import torch.distributed as dist
+    from custom_envs_amd.distributed import ShardedEnvs, shard_range
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    En, P, H, MB, T = 13, 4, 5, 30, 45
+    lo, hi = shard_range(En, world, rank)
+    eng = MultiOptEngine(hi - lo, 'func4', max_batches=MB, max_history=H)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    eng.set_stream(stream.cuda_stream)
+    shard = ShardedEnvs(eng, En, rank, world, slots=2, collective=True)
+    rs = np.random.RandomState(12)
+    lows = rs.uniform(-1.5, 1.5, En)
+    acts = np.stack([rs.uniform(lows[e], lows[e] + 1.5, (T, P)) for e in range(En)], 1)
+    acts = acts.astype(np.float32).reshape(T, En * P)
+    dacts = torch.from_numpy(np.ascontiguousarray(acts[:, lo * P:hi * P])).cuda()
+    keys = ('obs', 'done', 'episode_len', 'reward', 'info')
+    shard.reset(0)
+    got = {-1: {k: v.cpu().numpy() for k, v in shard.gather(0).snapshot().items() if k in keys}}
+    for t in range(T):
+        slot = t & 1 if pipelined else 0
+        shard.step(dacts[t], slot)
+        g = shard.gather(slot).snapshot()
+        torch.cuda.synchronize()
+        got[t] = {k: g[k].cpu().numpy() for k in keys}
+    if rank == 0:
+        np.savez(out_path, **{k: np.stack([got[t][k] for t in range(-1, T)]) for k in keys})
     eng.close()
     dist.destroy_process_group()
     return 0
