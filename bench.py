@@ -143,6 +143,10 @@ def parse(argv=None):
                    help='run the gather modes at world 1 too (a real 1-rank RCCL collective)')
     p.add_argument('--dry-run', action='store_true',
                    help='launcher + rank protocol only (gloo on CPU, no engine)')
+    p.add_argument('--one-gpu-rehearsal', action='store_true',
+                   help='N > 1 on a 1-GPU box: every rank on cuda:0, the collectives on gloo '
+                        '(RCCL puts no two ranks on one device); the whole N-rank path runs, '
+                        'the line says "rehearsal" and its rates are not N-GPU rates')
     p.add_argument('--profile-only', action='store_true',
                    help='run the timed steps only (for rocprofv3)')
     p.add_argument('--measure-traffic', action='store_true',
@@ -556,13 +560,17 @@ def main():
     dist = None
     if world > 1 or args.force_gather:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
+        dev_index = 0 if args.one_gpu_rehearsal else local_rank
+        torch.cuda.set_device(dev_index)
         if world == 1:
             os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
             os.environ.setdefault('MASTER_PORT', str(_free_port()))
             os.environ.setdefault('RANK', '0')
             os.environ.setdefault('WORLD_SIZE', '1')
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        if args.one_gpu_rehearsal:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
     else:
         torch.cuda.set_device(0)
     device = torch.cuda.current_device()
@@ -662,6 +670,8 @@ def main():
         torch.cuda.synchronize()
         graphs = {}
         try:
+            if dist.get_backend() != 'nccl':     # gloo (--one-gpu-rehearsal) cannot be captured
+                raise RuntimeError('backend %s has no graph capture' % dist.get_backend())
             for kind, fn in (('pipelined', run_gather_pipelined), ('serial', run_gather_serial)):
                 for n in sorted(set(gchunks(args.warmup) + gchunks(args.steps))):
                     g = torch.cuda.CUDAGraph()
@@ -674,7 +684,16 @@ def main():
         except Exception as exc:          # fall back to eager replays, say so
             gather_graph = 'eager (capture failed: %s)' % str(exc)[:200]
             graphs = {}
+            pending[0] = pending[1] = None       # handles from inside the failed capture
+            counter[0] = 0
             torch.cuda.synchronize()
+            # a stream whose capture was invalidated keeps failing launches:
+            # the eager replays run on a fresh one
+            stream = torch.cuda.Stream()
+            torch.cuda.set_stream(stream)
+            eng.set_stream(stream.cuda_stream)
+            print('bench: gather capture failed, eager gathers: %s' % str(exc)[:200],
+                  file=sys.stderr)
 
         def replayer(kind, eager):
             if not graphs:
@@ -774,6 +793,8 @@ def main():
         line['cpu_baseline'] = cpu
         if host_rate is not None:
             line['host_loop_env_steps_per_s'] = host_rate
+        if args.one_gpu_rehearsal:
+            line['rehearsal'] = '%d ranks on one GPU, collectives on gloo: not an N-GPU rate' % world
         print(json.dumps(line))
     eng.close()
     if dist is not None:

@@ -9,6 +9,12 @@
 
 #include "../../include/custom_envs_amd.h"
 
+// A sticky error left by an earlier failed operation that is not this
+// engine's (e.g. a caller's aborted stream capture) must not be reported as
+// the failure of the launches that follow: each entry point that checks
+// hipGetLastError() after its own launches clears the slot before them.
+#define CE_CLEAR_STALE_ERROR() ((void)hipGetLastError())
+
 #define CE_HIP(call)                                                              \
     do {                                                                          \
         hipError_t err_ = (call);                                                 \

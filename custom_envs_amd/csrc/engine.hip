@@ -399,6 +399,7 @@ bool complete(const ce_outputs *o, bool compact = false) {
 int do_step(ce_engine *e, const float *actions, const ce_outputs *out, uint32_t flags,
             bool sync) {
     if (!e) return fail(CE_EINVAL, "null engine");
+    CE_CLEAR_STALE_ERROR();
     if (!e->was_reset) return fail(CE_ESTATE, "step() before the first reset()");
     if (!actions) return fail(CE_EINVAL, "null actions");
     const size_t E = e->cfg.num_envs;
@@ -836,6 +837,7 @@ int ce_seed(ce_engine *e, const uint64_t *seeds, int32_t n) {
 
 int ce_reset(ce_engine *e, const ce_outputs *out, uint32_t flags) {
     if (!e) return fail(CE_EINVAL, "null engine");
+    CE_CLEAR_STALE_ERROR();
     if (flags & CE_PTR_DEVICE) {
         if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
         if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
@@ -897,6 +899,7 @@ int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
         if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
         if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
         const ce_outputs o = out ? *out : region_view(e, e->d_out);
+        CE_CLEAR_STALE_ERROR();
         const int rc = launch_steps(e, k, actions, stride, o);
         if (rc != CE_OK) return rc;
         CE_HIP(hipGetLastError());

@@ -144,6 +144,7 @@ void copy_out(const ce_multi_engine *e, const ce_multi_outputs &src, const ce_mu
 int do_step(ce_multi_engine *e, const float *actions, const ce_multi_outputs *out,
             uint32_t flags, bool sync) {
     if (!e) return fail(CE_EINVAL, "null engine");
+    CE_CLEAR_STALE_ERROR();
     if (!e->was_reset) return fail(CE_ESTATE, "step() before the first reset()");
     if (!actions) return fail(CE_EINVAL, "null actions");
     const size_t rows = static_cast<size_t>(e->cfg.num_envs) * e->cfg.n_params;
@@ -274,6 +275,7 @@ int ce_multi_set_stream(ce_multi_engine *e, void *stream) {
 
 int ce_multi_reset(ce_multi_engine *e, const ce_multi_outputs *out, uint32_t flags) {
     if (!e) return fail(CE_EINVAL, "null engine");
+    CE_CLEAR_STALE_ERROR();
     if (flags & CE_PTR_DEVICE) {
         if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
         const ce_multi_outputs o = out ? *out : region(e, e->d_out);

@@ -104,6 +104,7 @@ void copy_out(const ce_nn_engine *e, const ce_multi_outputs &src, const ce_multi
 int do_step(ce_nn_engine *e, const float *actions, const ce_multi_outputs *out, uint32_t flags,
             bool sync) {
     if (!e) return fail(CE_EINVAL, "null engine");
+    CE_CLEAR_STALE_ERROR();
     if (!e->was_reset) return fail(CE_ESTATE, "step() before the first reset()");
     if (!actions) return fail(CE_EINVAL, "null actions");
     const size_t rows = static_cast<size_t>(e->cfg.num_envs) * e->P;
@@ -393,6 +394,7 @@ int ce_nn_seed(ce_nn_engine *e, const uint64_t *seeds, int32_t n) {
 
 int ce_nn_reset(ce_nn_engine *e, const ce_multi_outputs *out, uint32_t flags) {
     if (!e) return fail(CE_EINVAL, "null engine");
+    CE_CLEAR_STALE_ERROR();
     if (!e->seeded) return fail(CE_ESTATE, "reset() before seed()");
     const size_t n = static_cast<size_t>(e->cfg.num_envs) * e->P * 3 * e->cfg.max_history;
     if (flags & CE_PTR_DEVICE) {
