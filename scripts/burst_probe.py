@@ -4,7 +4,11 @@ synchronize) against the GPU time between HIP events recorded on the engine
 stream right before the first and after the last step, and each kernel's
 own duration (events around every launch).  4096 envs, f64.
 
-    python scripts/burst_probe.py [--steps 20] [--reps 5]
+    python scripts/burst_probe.py [--steps 20] [--reps 5] [--preheat-ms 0]
+
+--preheat-ms X: before each rep, X ms of back-to-back steps and then an idle
+gap of --gap-ms (is a burst's per-kernel time a clock / power state that a
+busy GPU leaves behind?).
 """
 import argparse
 import json
@@ -21,6 +25,8 @@ def main():
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--reps', type=int, default=5)
     p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--preheat-ms', type=float, default=0.0)
+    p.add_argument('--gap-ms', type=float, default=0.0)
     args = p.parse_args()
     import torch
     from bench import lr_dataset
@@ -38,7 +44,15 @@ def main():
     run_k = eng.many_runner(K, acts, out)
     run_w = eng.many_runner(args.warmup, acts, out) if args.warmup else None
     torch.cuda.synchronize()
+    run_heat = eng.many_runner(250, torch.randn((250, E, eng.act_dim), device='cuda') * 0.01, out)
     for rep in range(args.reps):
+        if args.preheat_ms > 0:
+            t_h = time.perf_counter()
+            while (time.perf_counter() - t_h) * 1e3 < args.preheat_ms:
+                run_heat()
+                torch.cuda.synchronize()
+        if args.gap_ms > 0:
+            time.sleep(args.gap_ms / 1e3)
         if run_w:
             run_w()
         torch.cuda.synchronize()
@@ -51,7 +65,7 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         gpu_us = e0.elapsed_time(e1) * 1e3
-        print(json.dumps({'rep': rep, 'steps': K, 'wall_us': (t1 - t0) * 1e6,
+        print(json.dumps({'rep': rep, 'steps': K, 'preheat_ms': args.preheat_ms, 'gap_ms': args.gap_ms, 'wall_us': (t1 - t0) * 1e6,
                           'issue_us': (t_issue - t0) * 1e6, 'gpu_events_us': gpu_us,
                           'wall_us_per_step': (t1 - t0) * 1e6 / K,
                           'gpu_us_per_step': gpu_us / K}), flush=True)
