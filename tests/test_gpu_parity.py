@@ -363,3 +363,59 @@ def test_long_run_device_path_against_oracle(lr_dataset):
                                    atol=1e-14)
         assert st['step'][i] == T % 40
     eng.close()
+
+
+def test_config4_global_size_on_one_gpu(lr_dataset):
+    """Config 4's global batch (32,768 envs, BASELINE configs[3]) as ONE
+    engine: 2048 workgroups of the benchmark kernel, eight per CU.  Sampled
+    envs across the whole grid (the last lane of the last workgroup
+    included) against live oracle envs over 42 steps (one auto-reset), with
+    device-resident actions and outputs, plus a 4096-env engine seeded with
+    the same global indices giving the same bits for its envs (seeds =
+    global index: a shard of the batch reproduces the whole)."""
+    import torch
+    E, P, T = 32768, 20, 42
+    sample = [0, 17, 4095, 4096, 16383, 20000, 32766, 32767]
+    eng = _engine(lr_dataset, E)
+    assert eng.step_kernel == 'optimize_lr_mfma_kernel<3,3,4>'
+    eng.seed(list(range(E)))
+    part = _engine(lr_dataset, 4096)
+    part.seed(list(range(16384, 16384 + 4096)))
+    refs = {}
+    for i in sample:
+        env = OracleEnv(*lr_dataset)
+        env.seed(i)
+        env.reset()
+        refs[i] = env
+    out = eng.alloc_device_outputs()
+    pout = part.alloc_device_outputs()
+    eng.reset_device(out)
+    part.reset_device(pout)
+    gen = torch.Generator(device='cuda')
+    gen.manual_seed(4)
+    acts = torch.empty((E, P), dtype=torch.float32, device='cuda')
+    idx = torch.tensor(sample, device='cuda')
+    for t in range(T):
+        acts.normal_(0.0, 0.01, generator=gen)
+        torch.cuda.synchronize()
+        eng.step_device(acts, out)
+        part.step_device(acts[16384:16384 + 4096].contiguous(), pout)
+        eng.wait()
+        part.wait()
+        a = acts.index_select(0, idx).cpu().numpy()
+        got = {k: out[k].index_select(0, idx).cpu().numpy()
+               for k in ('obs', 'reward', 'done', 'episode_len', 'objective', 'accuracy')}
+        for j, i in enumerate(sample):
+            obs, rew, done, info = refs[i].step(a[j])
+            if done:
+                obs = refs[i].reset()
+            assert bool(got['done'][j]) == done, (i, t)
+            assert got['episode_len'][j] == info['episode']['l'], (i, t)
+            np.testing.assert_allclose(got['obs'][j], obs, rtol=F64_RTOL, atol=F64_ATOL,
+                                       err_msg='env %d step %d' % (i, t))
+            assert got['reward'][j] == pytest.approx(rew, rel=F64_RTOL), (i, t)
+            assert got['accuracy'][j] == np.float32(info['accuracy']), (i, t)
+        for k in ('obs', 'reward', 'episode_len'):
+            assert torch.equal(out[k][16384:16384 + 4096], pout[k]), (k, t)
+    eng.close()
+    part.close()
