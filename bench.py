@@ -149,12 +149,18 @@ def parse(argv=None):
                         'the line says "rehearsal" and its rates are not N-GPU rates')
     p.add_argument('--profile-only', action='store_true',
                    help='run the timed steps only (for rocprofv3)')
-    p.add_argument('--measure-traffic', action='store_true',
+    p.add_argument('--measure-traffic', action='store_true', default=None,
                    help='rank 0 at N = 1: measure roofline.traffic in this run (two rocprofv3 '
                         '--pmc passes of this workload as child processes, scripts/traffic.py); '
-                        'default: the committed profiles/<round>_traffic_<workload>.json')
+                        'the default when rocprofv3 is on PATH')
+    p.add_argument('--no-measure-traffic', dest='measure_traffic', action='store_false',
+                   help='take roofline.traffic from the committed '
+                        'profiles/<round>_traffic_<workload>.json instead')
     args = p.parse_args(argv)
     args.hidden = tuple(int(h) for h in str(args.hidden).split(',') if h)
+    if args.measure_traffic is None:
+        import shutil
+        args.measure_traffic = shutil.which('rocprofv3') is not None and not args.profile_only
     if args.workload == 'mnist' and '--steps' not in (argv or sys.argv):
         args.steps, args.warmup = 30, 3      # ~13 ms per step at 4096 envs
     if args.envs is None:
@@ -595,6 +601,14 @@ def main():
         out = shard.outs[0]
     else:
         out = eng.alloc_device_outputs()
+    # the optimize workload without a collective keeps every step's outputs:
+    # a [S] slab of output records (the device-resident rollout a learner
+    # consumes), written by ONE persistent launch per S steps where the
+    # engine has the K-step kernel (ce_step_many_strided)
+    slab = None
+    if args.workload == 'optimize' and shard is None and hasattr(eng, 'alloc_rollout'):
+        slab = eng.alloc_rollout(S)
+        out = {k: v[0] for k, v in slab[0].items() if k != '_buffer'}
     eng.reset_device(out)
 
     def chunks(k):
@@ -605,6 +619,8 @@ def main():
 
     def runner(n):
         # the engines with a pre-bound form skip the per-call argument checks
+        if slab is not None:
+            return eng.rollout_runner(n, actions, slab[0], slab[1])
         if hasattr(eng, 'many_runner'):
             return eng.many_runner(n, actions, out)
         return lambda: eng.step_many_device(n, actions, out)
@@ -644,7 +660,8 @@ def main():
 
     # hipGraphs for every chunk size the graph mode replays, built before any timing
     for n in sorted(set(chunks(args.warmup) + chunks(args.steps))):
-        eng.prepare_many_device(n, actions, out)
+        if slab is None:
+            eng.prepare_many_device(n, actions, out)
         runners[n] = runner(n)
     if args.profile_only:
         run_graph(args.warmup)
@@ -722,23 +739,32 @@ def main():
         primary(args.warmup)
         torch.cuda.synchronize()
         elapsed = _timed(torch, dist, primary, args.steps)
+        if slab is not None and getattr(eng, 'persistent', False):
+            # the same steps as one launch per step (the one-step kernel,
+            # what a closed-loop caller gets), timed the same way: the A/B
+            # beside `value`
+            eng.set_persistent(False)
+            runners.clear()
+            run_graph(args.warmup)
+            torch.cuda.synchronize()
+            modes['per_step_launch'] = _timed(torch, dist, run_graph, args.steps)
+            ev = launch_events(torch, stream, lambda: run_graph(S), S)
+            modes['per_step_launch_kernel_ms'] = ev[0]
+            eng.set_persistent(True)
+            runners.clear()
+            run_graph(args.warmup)
+            torch.cuda.synchronize()
 
     # live kernel duration: HIP events on the engine's stream (= torch's
     # current stream) around graph replays of S back-to-back step launches,
     # divided by S: the per-launch time on the stream, i.e. the kernel plus
     # its share of the inter-kernel boundary (rocprofv3's kernel-only average
     # is the same minus that gap; profiles/ holds both)
-    n_ev = 8
-    eng.step_many_device(S, actions, out)   # backlog: events then time the kernels, not the host
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
-    for i in range(n_ev):
-        starts[i].record(stream)
-        eng.step_many_device(S, actions, out)
-        ends[i].record(stream)
-    torch.cuda.synchronize()
-    times = [a.elapsed_time(b) / S for a, b in zip(starts, ends)]
-    kernel_ms, kernel_ms_mean = float(np.median(times)), float(np.mean(times))
+    if slab is not None:
+        kernel_ms, kernel_ms_mean = launch_events(torch, stream, lambda: run_graph(S), S)
+    else:
+        kernel_ms, kernel_ms_mean = launch_events(torch, stream,
+                                                  lambda: eng.step_many_device(S, actions, out), S)
     phase_ms = {}
     if mlp and rank == 0 and not eng.step_kernel.startswith('net<'):
         # each MLP kernel alone (CE_MLP_PHASES engines), same events method
@@ -778,7 +804,11 @@ def main():
         else:
             line = (multi_line if multi else optimize_line)(args, eng, world, E, S, elapsed,
                                                             kernel_ms, kernel_ms_mean, shard)
-        if modes:
+        if 'per_step_launch' in modes:
+            line['value_per_step_launch'] = world * E * args.steps / modes['per_step_launch']
+            line['ms_per_step_per_step_launch'] = modes['per_step_launch'] / args.steps * 1e3
+            line['roofline']['per_step_launch_kernel_ms'] = modes['per_step_launch_kernel_ms']
+        elif modes:
             units = world * E * args.steps
             line['value_gather_serial'] = units / modes['serial']
             line['value_gather_pipelined'] = units / modes['pipelined']
@@ -788,7 +818,8 @@ def main():
             line['gather_record'] = 'compact' if shard.compact else 'full'
             line['gather_mode'] = gather_mode
             line['gather_graph'] = gather_graph
-        bpe = line['roofline'].get('bytes_per_env_step')
+        bpe = line['roofline'].get('bytes_per_env_step', line['roofline'].get('hbm', {}).get(
+            'bytes_per_env_step'))
         line['roofline'].update(traffic_fields(args, eng, E, bpe if isinstance(bpe, (int, float)) else None))
         line['cpu_baseline'] = cpu
         if host_rate is not None:
@@ -800,6 +831,22 @@ def main():
     if dist is not None:
         dist.destroy_process_group()
     return 0
+
+
+def launch_events(torch, stream, fn, steps, n_ev=8):
+    """(median, mean) ms per step of `fn` (which issues `steps` steps on
+    `stream`) by HIP events on that stream: one warm call queued first so the
+    events time the GPU, not the host."""
+    fn()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
+    for i in range(n_ev):
+        starts[i].record(stream)
+        fn()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    times = [a.elapsed_time(b) / steps for a, b in zip(starts, ends)]
+    return float(np.median(times)), float(np.mean(times))
 
 
 def host_loop_rate(args, device, E):
@@ -841,8 +888,8 @@ def _common(args, world, E, S, elapsed, shard):
 # (scripts/traffic.py).  The committed summaries of this round are named here
 # and reported in roofline.traffic_source; --measure-traffic takes them in
 # the run instead.
-TRAFFIC_ROUND = 'r04'
-TRAFFIC_MARKER = {'optimize': 'optimize_lr_mfma_kernel', 'multi': 'multi_step_kernel',
+TRAFFIC_ROUND = 'r05'
+TRAFFIC_MARKER = {'optimize': 'optimize_lr_', 'multi': 'multi_step_kernel',
                   'mlp': 'mlp_step_kernel', 'net': 'net_finish_kernel',
                   'nn': 'nn_finalize_kernel', 'mnist': 'optimize_'}
 
@@ -853,10 +900,21 @@ def _traffic_name(args, eng):
     return args.workload
 
 
+def _traffic_steps(args):
+    """Steps per counted dispatch: the bench's launch size for the persistent
+    K-step kernel (every dispatch the same S steps), else 1."""
+    if args.workload == 'optimize' and int(os.environ.get('CE_PERSIST', '1')) != 0:
+        return max(1, min(args.graph_steps, args.steps))
+    return 1
+
+
 def _traffic_bench_args(args):
+    k = _traffic_steps(args)
     out = ['--workload', args.workload, '--envs', str(args.envs), '--profile-only',
-           '--steps', '6', '--warmup', '1', '--precision', args.precision,
-           '--batch-size', str(args.batch_size), '--hidden', ','.join(map(str, args.hidden))]
+           '--steps', str(max(k, 6)), '--warmup', str(k), '--graph-steps', str(args.graph_steps),
+           '--precision', args.precision]
+    if args.workload in ('mlp', 'nn'):
+        out += ['--batch-size', str(args.batch_size), '--hidden', ','.join(map(str, args.hidden))]
     return out
 
 
@@ -867,10 +925,11 @@ def traffic_fields(args, eng, E, bpe=None):
     import traffic as tr
     if args.measure_traffic and int(os.environ.get('WORLD_SIZE', '1')) == 1:
         try:
-            f, w = tr.collect(TRAFFIC_ROUND, name, _traffic_bench_args(args),
-                              os.path.join(ROOT, 'gpurun_out', 'traffic', name))
+            run_dir = os.path.join(ROOT, 'gpurun_out', 'traffic', name)
+            f, w = tr.collect(TRAFFIC_ROUND, name, _traffic_bench_args(args), run_dir)
             out, path = tr.summarize(f, w, TRAFFIC_MARKER[name], E, name, TRAFFIC_ROUND, bpe,
-                                     {'bench_args': ' '.join(_traffic_bench_args(args))})
+                                     {'bench_args': ' '.join(_traffic_bench_args(args))},
+                                     out_dir=run_dir, steps_per_dispatch=_traffic_steps(args))
             return {'traffic': out['hbm_bytes_per_step'],
                     'traffic_source': 'measured in this run: %s' % os.path.relpath(path, ROOT)}
         except Exception as exc:      # the committed file, and say why
@@ -891,10 +950,23 @@ def traffic_fields(args, eng, E, bpe=None):
 
 
 def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard):
+    """The headline line.  The dominant kernel is f64 work (MFMA for the two
+    GEMMs, VALU for the softmax: on gfx950 both issue at the same 78.6 TF/s
+    f64 rate and share the SIMD), so the roofline is the f64
+    pipe over the step's algorithmic FLOPs (SURVEY 8d: 2NFK + 2NFK + 5NK);
+    the HBM fraction of SURVEY 8d's byte count rides beside it."""
     P = eng.act_dim
     bpe = algorithmic_bytes_per_env_step(P, args.precision)
     achieved_gbs = bpe * E / (kernel_ms * 1e-3) / 1e9
     flops = 4 * 256 * P + 5 * 256 * 2
+    achieved_tf = flops * E / (kernel_ms * 1e-3) / 1e12
+    peak_tf = F64_VALU_PEAK_TFLOPS if args.precision == 'f64' else 157.3
+    kernel = getattr(eng, 'many_kernel', eng.step_kernel) if shard is None else eng.step_kernel
+    persistent = kernel.startswith('optimize_lr_persist_kernel')
+    # bytes a persistent launch of S steps moves per env-step: actions 4P and
+    # the outputs 4(2P+1) + 17 every step, the state (W, W0, G read; W, G
+    # written, f64; L, step r/w) once per launch
+    moved = 4 * P + 4 * (2 * P + 1) + 17 + (40 * P + 24) / S if persistent else bpe
     line = {'metric': METRIC}
     line.update(_common(args, world, E, S, elapsed, shard))
     line.update({
@@ -907,22 +979,27 @@ def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, sh
                         'auto-reset, device-resident actions/outputs' % E,
             'envs_per_gpu': E, 'global_envs': world * E, 'n_rows': 256,
             'n_features': 10, 'n_classes': 2, 'batch_size': 256,
-            'graph_steps': S, 'parallelism': 'env-sharded x%d (no collective)' % world
+            'steps_per_launch': S if persistent else 1,
+            'outputs': ('every step kept: a [%d]-record slab per launch' % S
+                        if persistent else 'every step into the same output buffers'),
+            'parallelism': 'env-sharded x%d (no collective)' % world
             if shard is None else 'env-sharded x%d + one RCCL all-gather of the packed '
             'outputs per step, pipelined over 2 buffers' % world,
         },
         'roofline': {
-            'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
-            'traffic': None,
-            'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
-            'kernel_ms_mean': kernel_ms_mean,
-            'kernel': 'ce::' + eng.step_kernel,
-            # the limiter is the f64/f32 VALU, not HBM:
-            # algorithmic FLOPs 2NFK (logits) + 2NFK (X^T(P-Y)) + 5NK
+            'bound': 'mfma', 'pipe': 'f64 (MFMA + VALU, one 78.6 TF/s rate on gfx950)',
+            'achieved': achieved_tf, 'peak': peak_tf, 'unit': 'TFLOP/s',
+            'frac': achieved_tf / peak_tf, 'traffic': None,
             'flops_per_env_step': flops,
-            'valu_tflops': flops * E / (kernel_ms * 1e-3) / 1e12,
-            'valu_peak_tflops': F64_VALU_PEAK_TFLOPS if args.precision == 'f64' else 157.3,
+            'kernel': 'ce::' + kernel, 'steps_per_launch': S if persistent else 1,
+            'kernel_ms_median': kernel_ms, 'kernel_ms_mean': kernel_ms_mean,
+            'kernel_ms_note': 'per step: HIP events around launches of S steps on the engine '
+                              'stream, divided by S',
+            'hbm': {'bytes_per_env_step': bpe, 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
+                    'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
+                    'bytes_per_env_step_moved': moved,
+                    'note': 'bytes_per_env_step is SURVEY 8d\'s count (state read+written every '
+                            'step, f64); bytes_per_env_step_moved is what the launch form moves'},
         },
     })
     return line

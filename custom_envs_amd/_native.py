@@ -15,7 +15,7 @@ if os.environ.get('CE_LIB') == 'diag':
 elif os.environ.get('CE_LIB'):
     LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd_%s.so' % os.environ['CE_LIB'])
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 CE_OK, CE_EINVAL, CE_EHIP, CE_ENOMEM, CE_ESTATE, CE_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
 CE_PROBLEM_SOFTMAX, CE_PROBLEM_MLP = 0, 1
 CE_F64, CE_F32 = 0, 1
@@ -26,10 +26,11 @@ STATUS_NAMES = {CE_EINVAL: 'CE_EINVAL', CE_EHIP: 'CE_EHIP', CE_ENOMEM: 'CE_ENOME
 
 # Every symbol include/custom_envs_amd.h declares.
 EXPORTS = (
-    'ce_abi_version', 'ce_last_error', 'ce_create', 'ce_destroy', 'ce_set_stream',
+    'ce_abi_version', 'ce_last_error', 'ce_stale_error_count', 'ce_stale_error_note', 'ce_create', 'ce_destroy', 'ce_set_stream',
     'ce_set_compact_outputs', 'ce_num_envs', 'ce_obs_dim', 'ce_act_dim', 'ce_seed', 'ce_seed_draws',
     'ce_seed_draws_mlp', 'ce_reset',
     'ce_step', 'ce_step_async', 'ce_wait', 'ce_step_many', 'ce_step_many_prepare',
+    'ce_step_many_strided', 'ce_set_persistent', 'ce_step_many_kernel',
     'ce_host_outputs', 'ce_step_kernel',
     'ce_get_state', 'ce_set_state',
     'ce_multi_create', 'ce_multi_destroy', 'ce_multi_set_stream', 'ce_multi_reset',
@@ -101,6 +102,8 @@ def _declare(lib):
     sig = {
         'ce_abi_version': ([], ctypes.c_int),
         'ce_last_error': ([], ctypes.c_char_p),
+        'ce_stale_error_count': ([], ctypes.c_int64),
+        'ce_stale_error_note': ([], ctypes.c_char_p),
         'ce_create': ([ctypes.POINTER(CeConfig), vp, vp, ctypes.POINTER(vp)], ctypes.c_int),
         'ce_destroy': ([vp], None),
         'ce_set_stream': ([vp, vp], ctypes.c_int),
@@ -117,6 +120,9 @@ def _declare(lib):
         'ce_wait': ([vp], ctypes.c_int),
         'ce_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeOutputs)], ctypes.c_int),
         'ce_step_many_prepare': ([vp, i32, vp, i64, ctypes.POINTER(CeOutputs)], ctypes.c_int),
+        'ce_step_many_strided': ([vp, i32, vp, i64, ctypes.POINTER(CeOutputs), i64], ctypes.c_int),
+        'ce_set_persistent': ([vp, i32], ctypes.c_int),
+        'ce_step_many_kernel': ([vp], ctypes.c_char_p),
         'ce_host_outputs': ([vp, ctypes.POINTER(CeOutputs)], ctypes.c_int),
         'ce_step_kernel': ([vp], ctypes.c_char_p),
         'ce_get_state': ([vp, ctypes.POINTER(CeState)], ctypes.c_int),
@@ -179,3 +185,22 @@ def check(rc, what):
         msg = load().ce_last_error().decode(errors='replace')
         raise NativeEngineError('%s: %s (%s)' % (what, msg, STATUS_NAMES.get(rc, rc)))
     return rc
+
+
+_stale_seen = [0]
+
+
+def warn_stale():
+    """Warn (once per new batch) when an entry point found a sticky HIP error
+    pending that an earlier, unrelated operation left behind and cleared it
+    (ce_stale_error_count / ce_stale_error_note): the failure is reported, not
+    lost.  Returns the process-wide count."""
+    lib = load()
+    n = int(lib.ce_stale_error_count())
+    if n > _stale_seen[0]:
+        import warnings
+        note = lib.ce_stale_error_note().decode(errors='replace')
+        warnings.warn('custom_envs_amd: %d stale HIP error(s) found pending and cleared; last: %s'
+                      % (n - _stale_seen[0], note), RuntimeWarning, stacklevel=2)
+        _stale_seen[0] = n
+    return n

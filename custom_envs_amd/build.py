@@ -29,8 +29,9 @@ def _hipcc():
 
 
 def sources():
-    return [os.path.join(CSRC, f) for f in ('engine.hip', 'optimize_mfma.hip', 'multi_engine.hip',
-                                            'multinn_engine.hip', 'net_engine.hip', 'seeding.cpp')]
+    return [os.path.join(CSRC, f) for f in ('engine.hip', 'optimize_mfma.hip', 'optimize_lr_persist.hip',
+                                            'multi_engine.hip', 'multinn_engine.hip', 'net_engine.hip',
+                                            'seeding.cpp')]
 
 
 def headers():
@@ -76,7 +77,8 @@ def _compile(out, tmp, defines, verbose):
         obj = os.path.join(tmp, os.path.basename(src) + '.o')
         if src.endswith('.hip'):
             cmd = [hipcc, '--offload-arch=' + ARCH, '-x', 'hip'] + common + ['-c', src, '-o', obj]
-            if os.path.basename(src) == 'optimize_mfma.hip' and 'CE_AGPR_FORM' not in defines:
+            if os.path.basename(src) in ('optimize_mfma.hip', 'optimize_lr_persist.hip') and \
+                    'CE_AGPR_FORM' not in defines:
                 # f64 MFMA results in VGPRs: the two-class kernel's softmax reads
                 # every forward C register, and the AGPR form cost 200
                 # v_accvgpr moves per wave

@@ -4,16 +4,46 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../../include/custom_envs_amd.h"
 
-// A sticky error left by an earlier failed operation that is not this
-// engine's (e.g. a caller's aborted stream capture) must not be reported as
-// the failure of the launches that follow: each entry point that checks
-// hipGetLastError() after its own launches clears the slot before them.
-#define CE_CLEAR_STALE_ERROR() ((void)hipGetLastError())
+namespace ce {
+
+// Sticky HIP errors found pending when an entry point starts.  Such an error
+// was left by an earlier failed operation that is not this call's (a
+// caller's aborted stream capture, another library's failed launch) and must
+// not be reported as the failure of the launches that follow, so the entry
+// point clears it -- but it is kept: counted, and its text noted, for
+// ce_stale_error_count / ce_stale_error_note (the Python side warns once).
+struct StaleErrors {
+    std::atomic<long long> count{0};
+    std::mutex mu;
+    std::string note;
+};
+inline StaleErrors &stale_errors() {
+    static StaleErrors s;
+    return s;
+}
+inline void note_stale(int code, const char *text, const char *where) {
+    StaleErrors &s = stale_errors();
+    s.count.fetch_add(1);
+    std::lock_guard<std::mutex> lock(s.mu);
+    s.note = std::string("HIP error ") + std::to_string(code) + " (" + (text ? text : "?") +
+             ") was pending at " + (where ? where : "?") + " and was cleared";
+}
+
+}  // namespace ce
+
+#define CE_CLEAR_STALE_ERROR()                                              \
+    do {                                                                    \
+        const hipError_t stale_ = hipGetLastError();                        \
+        if (stale_ != hipSuccess)                                           \
+            ce::note_stale(static_cast<int>(stale_), hipGetErrorString(stale_), __func__); \
+    } while (0)
 
 #define CE_HIP(call)                                                              \
     do {                                                                          \

@@ -134,6 +134,10 @@ struct ce_engine {
     int gen_cat = 1;          // CE_GEN_CAT=0: full batch on the one-env-per-wave kernel
     int lr_mode_cap = 3;      // CE_LR_MODE: cap on the two-class MFMA kernel's row-loop mode
     bool compact = false;     // ce_set_compact_outputs: device-pointer calls write the compact form
+    // the persistent K-step kernel (optimize_lr_persist.h): available for the
+    // shape, and chosen (ce_set_persistent; CE_PERSIST=0 at create turns it off)
+    bool persist = false, persist_on = true;
+    std::string many_name;    // what ce_step_many_kernel reports when persistent
     unsigned long long *diag = nullptr;   // CE_DIAG builds: per-wave phase stamps
 };
 
@@ -314,13 +318,36 @@ int launch(const ce_engine *e, bool reset, const float *act, const ce_outputs &o
     return CE_OK;
 }
 
-// k steps of every env, actions s * stride apart.
+// The outputs of step s of a strided run: every pointer out_step bytes per step.
+ce_outputs advance(const ce_outputs &o, int64_t bytes) {
+    auto adv = [bytes](auto *p) { return p ? reinterpret_cast<decltype(p)>(reinterpret_cast<char *>(p) + bytes) : p; };
+    ce_outputs r;
+    r.obs = adv(o.obs);
+    r.reward = adv(o.reward);
+    r.done = adv(o.done);
+    r.objective = adv(o.objective);
+    r.accuracy = adv(o.accuracy);
+    r.episode_len = adv(o.episode_len);
+    return r;
+}
+
+// k steps of every env, actions s * stride apart, outputs s * out_step bytes
+// apart (one launch per step).
 int launch_steps(const ce_engine *e, int k, const float *actions, int64_t stride,
-                 const ce_outputs &o) {
+                 const ce_outputs &o, int64_t out_step = 0) {
     for (int s = 0; s < k; ++s) {
-        const int rc = launch(e, false, actions + s * stride, o, e->stream, e->compact);
+        const int rc = launch(e, false, actions + s * stride, out_step ? advance(o, s * out_step) : o,
+                              e->stream, e->compact);
         if (rc != CE_OK) return rc;
     }
+    return CE_OK;
+}
+
+// The k steps as ONE launch of the persistent kernel (optimize_lr_persist.h).
+int launch_persist(const ce_engine *e, int k, const float *actions, int64_t stride,
+                   const ce_outputs &o, int64_t out_step) {
+    const auto a = make_args<double>(e, actions, o, e->compact);
+    ce::lr_launch_persist(a, k, stride, out_step, e->stream);
     return CE_OK;
 }
 
@@ -677,6 +704,9 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
             return bail(fail(CE_EHIP, "ce_create: dataset upload failed"));
         e->kernel_name = ce::lr_kernel_name(cfg->num_envs, cfg->n_rows, cfg->n_features,
                                             e->lr_waves, e->lr_mode_cap);
+        e->persist = ce::lr_persist_ok(cfg->n_rows);
+        if (e->persist) e->many_name = ce::lr_persist_name(cfg->n_rows, cfg->n_features);
+        if (const char *pe = std::getenv("CE_PERSIST")) e->persist_on = pe[0] != '0';
     } else if (e->gen_ft) {
         // [Npad][RS] float64: F features, zeros to 16 FT + 1, the label as a
         // double in the last column; rows N..Npad-1 are zeros with label -1
@@ -891,8 +921,40 @@ int many_graph(ce_engine *e, int32_t k, const float *actions, int64_t stride,
 
 }  // namespace
 
+namespace {
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// the arguments every k-step form checks
+int many_args_ok(const ce_engine *e, int32_t k, const float *actions, int64_t stride,
+                 const ce_outputs *out) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
+    if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "ce_step_many: bad arguments");
+    if (e->compact && !out) return fail(CE_EINVAL, "compact outputs need caller buffers");
+    if (out && !complete(out, e->compact)) return fail(CE_EINVAL, "device outputs must all be set");
+    return CE_OK;
+}
+
+bool use_persist(const ce_engine *e, const ce_outputs &o) {
+    return e->persist && e->persist_on && aligned16(o.obs);
+}
+
+}  // namespace
+
 int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
                  const ce_outputs *out) {
+    if (e && e->persist && e->persist_on) {
+        const int rc = many_args_ok(e, k, actions, stride, out);
+        if (rc != CE_OK) return rc;
+        const ce_outputs o = out ? *out : region_view(e, e->d_out);
+        if (use_persist(e, o)) {
+            CE_CLEAR_STALE_ERROR();
+            (void)launch_persist(e, k, actions, stride, o, 0);
+            CE_HIP(hipGetLastError());
+            return CE_OK;
+        }
+    }
     if (e && k <= e->many_direct) {
         if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
         if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "ce_step_many: bad arguments");
@@ -914,8 +976,58 @@ int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
 
 int ce_step_many_prepare(ce_engine *e, int32_t k, const float *actions, int64_t stride,
                          const ce_outputs *out) {
+    if (e && e->persist && e->persist_on) {   // one launch: nothing to instantiate
+        const int rc = many_args_ok(e, k, actions, stride, out);
+        if (rc != CE_OK) return rc;
+        const ce_outputs o = out ? *out : region_view(e, e->d_out);
+        if (use_persist(e, o)) return CE_OK;
+    }
     hipGraphExec_t exec;
     return many_graph(e, k, actions, stride, out, &exec);
+}
+
+int ce_step_many_strided(ce_engine *e, int32_t k, const float *actions, int64_t stride,
+                         const ce_outputs *out, int64_t out_step) {
+    int rc = many_args_ok(e, k, actions, stride, out);
+    if (rc != CE_OK) return rc;
+    if (!out) return fail(CE_EINVAL, "ce_step_many_strided: needs caller output buffers");
+    if (out_step < 0 || out_step % 16 != 0 || !aligned16(out->obs))
+        return fail(CE_EINVAL, "ce_step_many_strided: obs must be 16-byte aligned and "
+                               "out_step_bytes a non-negative multiple of 16");
+    CE_CLEAR_STALE_ERROR();
+    rc = use_persist(e, *out) ? launch_persist(e, k, actions, stride, *out, out_step)
+                              : launch_steps(e, k, actions, stride, *out, out_step);
+    if (rc != CE_OK) return rc;
+    CE_HIP(hipGetLastError());
+    return CE_OK;
+}
+
+int ce_set_persistent(ce_engine *e, int32_t on) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    e->persist_on = on != 0;
+    return CE_OK;
+}
+
+const char *ce_step_many_kernel(const ce_engine *e) {
+    if (!e) return "";
+    if (e->persist && e->persist_on) return e->many_name.c_str();
+    return ce_step_kernel(e);
+}
+
+int64_t ce_stale_error_count(void) { return ce::stale_errors().count.load(); }
+
+const char *ce_stale_error_note(void) {
+    static thread_local std::string copy;
+    std::lock_guard<std::mutex> lock(ce::stale_errors().mu);
+    copy = ce::stale_errors().note;
+    return copy.c_str();
+}
+
+// Test hook (not part of include/custom_envs_amd.h): record a stale error as
+// an entry point would, so the bookkeeping is testable without a GPU.
+int ce_test_note_stale_error(int32_t code) {
+    ce::note_stale(code, "injected by a test", "ce_test_note_stale_error");
+    return CE_OK;
 }
 
 const char *ce_step_kernel(const ce_engine *e) {

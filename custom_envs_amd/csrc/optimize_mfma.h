@@ -36,4 +36,14 @@ void lr_launch_step(const StepArgs<double> &a, hipStream_t stream);
 // "optimize_lr_mfma_kernel<NKF,MODE,W>"
 std::string lr_kernel_name(int n_envs, int n_rows, int n_features, int lr_waves, int mode_cap);
 
+// K steps in one launch (optimize_lr_persist.h, optimize_lr_persist.hip):
+// the same two-class full-batch shapes with N <= 512 rows.  Step t reads
+// actions a.act + t * act_stride and writes its outputs out_step bytes past
+// step t - 1's (0: every step into the same record).
+bool lr_persist_ok(int n_rows);
+void lr_launch_persist(const StepArgs<double> &a, int k, long long act_stride, long long out_step,
+                       hipStream_t stream);
+// "optimize_lr_persist_kernel<NKF,TPW,PAD>"
+std::string lr_persist_name(int n_rows, int n_features);
+
 }  // namespace ce

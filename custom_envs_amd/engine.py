@@ -114,6 +114,7 @@ class OptimizeEngine:
         self._h = handle
         self.act_dim = lib.ce_act_dim(handle)
         self.step_kernel = lib.ce_step_kernel(handle).decode()
+        self.many_kernel = lib.ce_step_many_kernel(handle).decode()
         self.obs_dim = lib.ce_obs_dim(handle)
         view = CeOutputs()
         check(lib.ce_host_outputs(handle, ctypes.byref(view)), 'ce_host_outputs')
@@ -147,6 +148,7 @@ class OptimizeEngine:
     # --------------------------------------------------------------- host mode
     def reset(self):
         check(self._lib.ce_reset(self._h, None, 0), 'ce_reset')
+        _native.warn_stale()
         return self._host['obs'].copy()
 
     def step_async(self, actions):
@@ -160,6 +162,7 @@ class OptimizeEngine:
         """Return views of the pinned outputs (valid until the next step)."""
         check(self._lib.ce_wait(self._h), 'ce_wait')
         self._pending = None
+        _native.warn_stale()
         return self._host
 
     def step(self, actions):
@@ -221,7 +224,7 @@ class OptimizeEngine:
         return {name: torch.empty((self.num_envs * rows,) + tail, dtype=dtype, device=dev)
                 for name, dtype, rows, tail in self.output_fields()}
 
-    def _check_device_tensors(self, actions, out, steps=1):
+    def _check_device_tensors(self, actions, out, steps=1, strided=False):
         if actions.dtype.itemsize != 4 or not actions.is_contiguous():
             raise ValueError('actions must be a contiguous float32 device tensor')
         if actions.numel() < steps * self.num_envs * self.act_dim:
@@ -229,6 +232,8 @@ class OptimizeEngine:
         for key, t in out.items():
             if not t.is_contiguous():
                 raise ValueError('output %s must be contiguous' % key)
+            if strided and t.data_ptr() % 16:
+                raise ValueError('output %s must be 16-byte aligned' % key)
         if self.compact:
             if 'obs_tail' not in out or out['obs_tail'].numel() != self.num_envs * (self.act_dim + 1):
                 raise ValueError('compact outputs need obs_tail of [E][P + 1]')
@@ -239,6 +244,7 @@ class OptimizeEngine:
         o = self._outputs(out)
         check(self._lib.ce_reset(self._h, ctypes.byref(o), _native.CE_PTR_DEVICE),
               'ce_reset')
+        _native.warn_stale()
 
     def step_device(self, actions, out):
         """Stream-ordered step from a device action tensor into device outputs."""
@@ -283,6 +289,75 @@ class OptimizeEngine:
 
     def wait(self):
         check(self._lib.ce_wait(self._h), 'ce_wait')
+        _native.warn_stale()
+
+    # ------------------------------------------------- K steps in one launch
+    def set_persistent(self, on=True):
+        """K-step calls (step_many_device, rollout_device) as ONE launch of
+        the persistent kernel where this engine has one (``many_kernel``
+        names it), or one launch per step (on=False, the A/B form)."""
+        check(self._lib.ce_set_persistent(self._h, 1 if on else 0), 'ce_set_persistent')
+        self.many_kernel = self._lib.ce_step_many_kernel(self._h).decode()
+
+    @property
+    def persistent(self):
+        return self.many_kernel.startswith('optimize_lr_persist_kernel')
+
+    def alloc_rollout(self, k, torch_device=None):
+        """A [k] array of output records for ``rollout_device``: one byte
+        buffer whose record t holds step t's fields (256-B aligned segments).
+        Returns (fields, record_bytes): fields maps each output name to a
+        (k, E, ...) view of the buffer."""
+        import torch
+        dev = torch_device or torch.device('cuda', self.device)
+        offs, off = {}, 0
+        spec = self.output_fields()
+        for name, dtype, rows, tail in spec:
+            n = self.num_envs * rows * int(np.prod(tail, dtype=np.int64)) * \
+                torch.empty((), dtype=dtype).element_size()
+            offs[name] = off
+            off += -(-n // 256) * 256
+        rec = off
+        buf = torch.zeros(int(k) * rec, dtype=torch.uint8, device=dev)
+        fields = {}
+        for name, dtype, rows, tail in spec:
+            size = torch.empty((), dtype=dtype).element_size()
+            inner = (self.num_envs * rows,) + tuple(tail)
+            strides = [1] * len(inner)
+            for i in range(len(inner) - 2, -1, -1):
+                strides[i] = strides[i + 1] * inner[i + 1]
+            fields[name] = buf.view(dtype).as_strided((int(k),) + inner, (rec // size,) + tuple(strides),
+                                                      offs[name] // size)
+        fields['_buffer'] = buf
+        return fields, rec
+
+    def rollout_device(self, k, actions, fields, record_bytes, per_step_actions=True):
+        """k stream-ordered steps keeping every step's outputs: step t reads
+        actions[t] and writes record t of ``fields`` (``alloc_rollout``)
+        (``ce_step_many_strided``).  One launch where ``persistent``."""
+        self._check_device_tensors(actions, {n: v[0] for n, v in fields.items() if n != '_buffer'},
+                                   k if per_step_actions else 1, strided=True)
+        stride = self.num_envs * self.act_dim if per_step_actions else 0
+        o = self._outputs({n: v[0] for n, v in fields.items() if n != '_buffer'})
+        check(self._lib.ce_step_many_strided(self._h, int(k), actions.data_ptr(), stride,
+                                             ctypes.byref(o), int(record_bytes)),
+              'ce_step_many_strided')
+
+    def rollout_runner(self, k, actions, fields, record_bytes, per_step_actions=True):
+        """rollout_device bound once (see many_runner)."""
+        first = {n: v[0] for n, v in fields.items() if n != '_buffer'}
+        self._check_device_tensors(actions, first, k if per_step_actions else 1, strided=True)
+        stride = self.num_envs * self.act_dim if per_step_actions else 0
+        o = self._outputs(first)
+        fn, h, ap, ref, kk, rb = (self._lib.ce_step_many_strided, self._h, actions.data_ptr(),
+                                  ctypes.byref(o), int(k), int(record_bytes))
+
+        def run():
+            rc = fn(h, kk, ap, stride, ref, rb)
+            if rc:
+                check(rc, 'ce_step_many_strided')
+        run.keep = (actions, fields, o)
+        return run
 
     # ------------------------------------------------------------------ state
     def get_state(self):

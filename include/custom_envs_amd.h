@@ -27,6 +27,13 @@
  *                  instantiate + upload that hipGraph without running it (graphs
  *                  are cached per (k, actions, stride, outputs, stream), so a
  *                  timed region never captures)
+ *   ce_step_many_strided
+ *                  K consecutive VecEnv.step calls in ONE persistent launch
+ *                  (concurrentvecenv.py:94-107 x K over optimize.py:69-100 and
+ *                  the utils_venv.py:31 auto-reset), step t's outputs into
+ *                  record t of a [K] output slab (a device-resident rollout)
+ *   ce_set_persistent / ce_step_many_kernel
+ *                  choose / name the K-step launch form (no reference analogue)
  *   ce_get_state / ce_set_state
  *                  the per-env attributes model.weights, loss_hist, grad_hist,
  *                  current_step (optimize.py:45-50, baseenvironment.py:18)
@@ -79,7 +86,7 @@
 extern "C" {
 #endif
 
-#define CE_ABI_VERSION 4
+#define CE_ABI_VERSION 5
 
 typedef struct ce_engine ce_engine;
 
@@ -158,6 +165,12 @@ typedef struct ce_state {
 
 int ce_abi_version(void);
 const char *ce_last_error(void);
+/* Sticky HIP errors an entry point found pending when it started (left by
+ * another component, e.g. a caller's aborted stream capture) and cleared so
+ * that they are not reported as its own failure: how many so far in this
+ * process, and a note naming the last one ("" if none). */
+int64_t ce_stale_error_count(void);
+const char *ce_stale_error_note(void);
 
 int ce_create(const ce_config *cfg, const double *features /* [N][F] */,
               const int32_t *labels /* [N] class index */, ce_engine **out);
@@ -200,6 +213,27 @@ int ce_step_many(ce_engine *eng, int32_t k, const float *actions,
                  const ce_outputs *out /* device pointers */);
 int ce_step_many_prepare(ce_engine *eng, int32_t k, const float *actions,
                          int64_t action_step_stride, const ce_outputs *out);
+/* K steps whose outputs are kept: step t reads actions + t * action_step_stride
+ * and writes every output of `out` (device pointers) advanced by
+ * t * out_step_bytes -- a [K] array of output records, e.g. one buffer per
+ * field of [K][E] rows (out_step_bytes = that field's E rows) or one packed
+ * record per step.  out_step_bytes == 0 overwrites the same outputs every step
+ * (ce_step_many).  Where the engine has a persistent kernel (two-class,
+ * B == N, float64, n_rows <= 512: ce_step_many_kernel names it) the K steps
+ * are ONE launch: the per-env state stays in registers across them and is
+ * stored once; otherwise K step launches.  Stream-ordered, asynchronous.
+ * obs must be 16-byte aligned and out_step_bytes a multiple of 16, else
+ * CE_EINVAL. */
+int ce_step_many_strided(ce_engine *eng, int32_t k, const float *actions,
+                         int64_t action_step_stride, const ce_outputs *out,
+                         int64_t out_step_bytes);
+/* on = 1 (default; CE_PERSIST=0 in the environment at ce_create makes it 0):
+ * ce_step_many and ce_step_many_strided use the persistent K-step kernel where
+ * the engine has one; on = 0: one launch per step (the A/B form). */
+int ce_set_persistent(ce_engine *eng, int32_t on);
+/* The kernel ce_step_many runs: "optimize_lr_persist_kernel<NKF,TPW,PAD>" when
+ * persistent, else ce_step_kernel's name. */
+const char *ce_step_many_kernel(const ce_engine *eng);
 
 /* Pinned host buffers holding the last host-mode outputs (zero-copy views). */
 int ce_host_outputs(ce_engine *eng, ce_outputs *view);

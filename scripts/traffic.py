@@ -14,8 +14,11 @@ a wide coalesced read, so it is doubled -- narrower accesses are
 uncalibrated, and the doubling then overstates them) and sums the kernels
 of one step: bytes per step = sum over kernels of mean bytes per dispatch x
 dispatches per step, dispatches per step = dispatches / the step kernel's
-dispatches.  Writes profiles/<round>_traffic_<name>.json, which bench.py
-names in ``roofline.traffic_source``.
+dispatches, divided by ``steps_per_dispatch`` when the step kernel runs
+several steps per launch (the persistent K-step kernel).  The CLI writes
+profiles/<round>_traffic_<name>.json (the committed evidence); bench.py's
+in-run measurement writes under gpurun_out/traffic/ and names that file in
+``roofline.traffic_source``.
 """
 import argparse
 import collections
@@ -46,13 +49,18 @@ def _short(name):
     return name.replace('void ', '')
 
 
-def summarize(src_fetch, src_write, step_kernel, envs, name, rnd, bpe=None, extra=None):
+def summarize(src_fetch, src_write, step_kernel, envs, name, rnd, bpe=None, extra=None,
+              out_dir=None, steps_per_dispatch=1):
+    """Bytes per step from the two counter passes.  Raises ValueError when
+    no dispatch of `step_kernel` was counted (a caller catching Exception
+    keeps going); writes <out_dir>/<rnd>_traffic_<name>.json (default: the
+    CE_TRAFFIC_OUT directory, else profiles/)."""
     fetch = _counters(src_fetch, 'FETCH_SIZE')
     write = _counters(src_write, 'WRITE_SIZE')
     marker = [k for k in fetch if step_kernel in k]
     if not marker:
-        raise SystemExit('no dispatch of %r in the FETCH_SIZE pass' % step_kernel)
-    steps = len(fetch[marker[0]])
+        raise ValueError('no dispatch of %r in the FETCH_SIZE pass' % step_kernel)
+    steps = len(fetch[marker[0]]) * steps_per_dispatch
     wsteps = sum(len(v) for k, v in write.items() if step_kernel in k)
     kernels = {}
     total_r = total_w = 0.0
@@ -61,13 +69,14 @@ def summarize(src_fetch, src_write, step_kernel, envs, name, rnd, bpe=None, extr
         wr = write.get(k, [])
         r_mean = 2.0 * 1024 * sum(rd) / len(rd) if rd else 0.0
         w_mean = 1024 * sum(wr) / len(wr) if wr else 0.0
-        per_step = len(rd) / steps if rd else (len(wr) / wsteps if wsteps else 0.0)
+        per_step = (len(rd) / steps if rd else
+                    (len(wr) / (wsteps * steps_per_dispatch) if wsteps else 0.0))
         kernels[_short(k)] = {'read_bytes_per_dispatch': r_mean, 'write_bytes_per_dispatch': w_mean,
                               'dispatches_per_step': per_step}
         total_r += r_mean * per_step
         total_w += w_mean * per_step
     out = {'round': rnd, 'name': name, 'envs': envs, 'step_kernel': step_kernel,
-           'steps_profiled': steps, 'hbm_read_bytes_per_step': total_r,
+           'steps_profiled': steps, 'steps_per_dispatch': steps_per_dispatch, 'hbm_read_bytes_per_step': total_r,
            'hbm_write_bytes_per_step': total_w, 'hbm_bytes_per_step': total_r + total_w,
            'kernels': kernels,
            'method': 'rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs; '
@@ -80,7 +89,7 @@ def summarize(src_fetch, src_write, step_kernel, envs, name, rnd, bpe=None, extr
         out.update(extra)
     # CE_TRAFFIC_OUT: where to write (a GPU box returns only gpurun_out/;
     # the committed copies live in profiles/)
-    out_dir = os.environ.get('CE_TRAFFIC_OUT', os.path.join(ROOT, 'profiles'))
+    out_dir = out_dir or os.environ.get('CE_TRAFFIC_OUT', os.path.join(ROOT, 'profiles'))
     os.makedirs(out_dir, exist_ok=True)
     path = os.path.join(out_dir, '%s_traffic_%s.json' % (rnd, name))
     with open(path, 'w') as fh:
@@ -114,6 +123,7 @@ def main():
     p.add_argument('--step-kernel', required=True, help='substring of the once-per-step kernel')
     p.add_argument('--envs', type=int, required=True)
     p.add_argument('--bytes-per-env-step', type=float, default=None)
+    p.add_argument('--steps-per-dispatch', type=int, default=1)
     p.add_argument('--src', default=None, help='summarize: directory with fetch_size/ write_size/')
     p.add_argument('--out', default=os.path.join(ROOT, 'gpurun_out', 'traffic'))
     p.add_argument('bench_args', nargs=argparse.REMAINDER)
@@ -125,8 +135,12 @@ def main():
     else:
         src = args.src or os.path.join(args.out, args.name)
         f, w = os.path.join(src, 'fetch_size'), os.path.join(src, 'write_size')
-    out, path = summarize(f, w, args.step_kernel, args.envs, args.name, args.round,
-                          args.bytes_per_env_step, {'bench_args': ' '.join(bench_args)})
+    try:
+        out, path = summarize(f, w, args.step_kernel, args.envs, args.name, args.round,
+                              args.bytes_per_env_step, {'bench_args': ' '.join(bench_args)},
+                              steps_per_dispatch=args.steps_per_dispatch)
+    except ValueError as exc:
+        raise SystemExit(str(exc))
     print(path)
     print(json.dumps({k: v for k, v in out.items() if k != 'kernels'}, indent=1, sort_keys=True))
 

@@ -208,13 +208,17 @@ def test_single_env_api_matches_oracle(lr_dataset):
     env.close()
 
 
-@pytest.mark.parametrize('many_direct,bound', [('32', False), ('0', False), ('32', True)])
-def test_device_path_matches_host_path(lr_dataset, many_direct, bound, monkeypatch):
+@pytest.mark.parametrize('many_direct,bound,persist', [('32', False, '0'), ('0', False, '0'),
+                                                       ('32', True, '0'), ('32', False, '1'),
+                                                       ('32', True, '1')])
+def test_device_path_matches_host_path(lr_dataset, many_direct, bound, persist, monkeypatch):
     """ce_step_many as plain launches (k <= CE_MANY_DIRECT, default 32), as a
-    replayed hipGraph (CE_MANY_DIRECT=0) and through the pre-bound
-    many_runner give the host path's bits."""
+    replayed hipGraph (CE_MANY_DIRECT=0), through the pre-bound many_runner,
+    and as ONE persistent launch (CE_PERSIST=1, the default) give the host
+    path's bits."""
     import torch
     monkeypatch.setenv('CE_MANY_DIRECT', many_direct)
+    monkeypatch.setenv('CE_PERSIST', persist)
     E, P, K = 512, 20, 12
     acts = np.random.RandomState(4).normal(0, 0.01, (K, E, P)).astype(np.float32)
     host = _engine(lr_dataset, E)
@@ -223,6 +227,7 @@ def test_device_path_matches_host_path(lr_dataset, many_direct, bound, monkeypat
     for t in range(K):
         ref = host.step(acts[t])
     dev = _engine(lr_dataset, E)
+    assert dev.persistent == (persist == '1')
     dev.seed(0)
     stream = torch.cuda.Stream()
     with torch.cuda.stream(stream):
