@@ -131,7 +131,11 @@ def parse(argv=None):
     p.add_argument('--hidden', default='64',
                    help='mlp workload: hidden widths, e.g. 256,256 (create_neural_net default)')
     p.add_argument('--batch-size', type=int, default=32, help='mlp workload: minibatch rows')
-    p.add_argument('--graph-steps', type=int, default=250, help='steps per hipGraph replay')
+    p.add_argument('--graph-steps', type=int, default=250,
+                   help='steps per launch (persistent kernel) or per hipGraph replay')
+    p.add_argument('--chunk-steps', type=int, default=10,
+                   help='N > 1, optimize: steps per rollout launch and per all-gather in the '
+                        'chunk schedule')
     p.add_argument('--no-gather', action='store_true',
                    help='N > 1: no per-step all-gather in the headline value')
     p.add_argument('--gather', action='store_true',
@@ -597,7 +601,11 @@ def main():
     if gather_modes:
         from custom_envs_amd.distributed import ShardedEnvs
         # two packed buffers: the engine writes straight into them (no packing kernels)
-        shard = ShardedEnvs(eng, world * E, rank, world, slots=2, collective=True)
+        # the chunk schedule where the engine runs K steps per launch: each
+        # slot holds K step records, gathered by ONE collective
+        chunk = (max(1, min(args.chunk_steps, args.steps))
+                 if args.workload == 'optimize' and getattr(eng, 'persistent', False) else 1)
+        shard = ShardedEnvs(eng, world * E, rank, world, slots=2, collective=True, chunk=chunk)
         out = shard.outs[0]
     else:
         out = eng.alloc_device_outputs()
@@ -658,6 +666,40 @@ def main():
             shard.gather(0)
             counter[0] += 1
 
+    # the chunk schedule: ONE persistent launch of C steps into
+    # a C-record slot, then ONE all-gather of the slot; pipelined, chunk c's
+    # gather runs on RCCL's stream while chunk c + 1's launch writes the
+    # other slot (the engine stream waits for the gather that read a slot
+    # before rewriting it)
+    chunk_runners = {}
+    C = shard.chunk if shard is not None else 1
+
+    def cchunks(k):
+        return [C] * (k // C) + ([k % C] if k % C else [])
+
+    def chunk_launch(slot, n):
+        if (slot, n) not in chunk_runners:
+            chunk_runners[slot, n] = shard.rollout_runner(actions[:n], slot, n)
+        chunk_runners[slot, n]()
+
+    def run_chunk_pipelined(k):
+        for n in cchunks(k):
+            slot = counter[0] & 1
+            if pending[slot] is not None:
+                pending[slot].wait()
+            chunk_launch(slot, n)
+            _, pending[slot] = shard.gather_chunk(slot, async_op=True, k=n)
+            counter[0] += 1
+        for slot in (0, 1):
+            if pending[slot] is not None:
+                pending[slot].wait()
+                pending[slot] = None
+
+    def run_chunk_serial(k):
+        for n in cchunks(k):
+            chunk_launch(0, n)
+            shard.gather_chunk(0, k=n)
+
     # hipGraphs for every chunk size the graph mode replays, built before any timing
     for n in sorted(set(chunks(args.warmup) + chunks(args.steps))):
         if slab is None:
@@ -684,12 +726,17 @@ def main():
 
         run_gather_pipelined(max(args.warmup, 4))     # communicators up before capture
         run_gather_serial(2)
+        kinds = [('pipelined', run_gather_pipelined), ('serial', run_gather_serial)]
+        if C > 1:
+            run_chunk_pipelined(2 * C + 1)
+            run_chunk_serial(C + 1)
+            kinds += [('chunk_pipelined', run_chunk_pipelined), ('chunk_serial', run_chunk_serial)]
         torch.cuda.synchronize()
         graphs = {}
         try:
             if dist.get_backend() != 'nccl':     # gloo (--one-gpu-rehearsal) cannot be captured
                 raise RuntimeError('backend %s has no graph capture' % dist.get_backend())
-            for kind, fn in (('pipelined', run_gather_pipelined), ('serial', run_gather_serial)):
+            for kind, fn in kinds:
                 for n in sorted(set(gchunks(args.warmup) + gchunks(args.steps))):
                     g = torch.cuda.CUDAGraph()
                     counter[0] = 0
@@ -703,6 +750,7 @@ def main():
             graphs = {}
             pending[0] = pending[1] = None       # handles from inside the failed capture
             counter[0] = 0
+            chunk_runners.clear()
             torch.cuda.synchronize()
             # a stream whose capture was invalidated keeps failing launches:
             # the eager replays run on a fresh one
@@ -721,18 +769,20 @@ def main():
                     graphs[kind, n].replay()
             return run
 
-        run_pipe = replayer('pipelined', run_gather_pipelined)
-        run_ser = replayer('serial', run_gather_serial)
-        run_pipe(args.warmup)
-        modes['pipelined'] = _timed(torch, dist, run_pipe, args.steps)
-        run_ser(args.warmup)
-        modes['serial'] = _timed(torch, dist, run_ser, args.steps)
+        for kind, fn in kinds:
+            run = replayer(kind, fn)
+            run(args.warmup)
+            modes[kind] = _timed(torch, dist, run, args.steps)
         run_graph(args.warmup)
         modes['no_gather'] = _timed(torch, dist, run_graph, args.steps)
-        # both schedules run every step AND its all-gather inside the timed
-        # region; `value` is the closed-loop serial one (a learner acts on
-        # step t's outputs before step t + 1), the pipelined rate rides along
-        gather_mode = 'serial'
+        # every schedule runs every step AND the all-gather of its outputs
+        # inside the timed region.  `value`: the chunk schedule where the
+        # engine has the K-step launch (the actions of a chunk are device-
+        # resident before it starts -- the open-loop rollout a persistent
+        # launch serves; the gather of chunk c overlaps chunk c + 1), else
+        # the per-step serial schedule (a closed-loop learner acting on step
+        # t's outputs before step t + 1), which rides along either way
+        gather_mode = 'chunk_pipelined' if C > 1 else 'serial'
         elapsed = modes[gather_mode]
     else:
         primary = run_graph
@@ -810,9 +860,13 @@ def main():
             line['roofline']['per_step_launch_kernel_ms'] = modes['per_step_launch_kernel_ms']
         elif modes:
             units = world * E * args.steps
-            line['value_gather_serial'] = units / modes['serial']
-            line['value_gather_pipelined'] = units / modes['pipelined']
+            line['value_gather_serial_per_step'] = units / modes['serial']
+            line['value_gather_pipelined_per_step'] = units / modes['pipelined']
+            for kind in ('chunk_pipelined', 'chunk_serial'):
+                if kind in modes:
+                    line['value_gather_' + kind] = units / modes[kind]
             line['value_no_gather'] = units / modes['no_gather']
+            line['gather_chunk_steps'] = C
             line['ms_per_step_modes'] = {k: v / args.steps * 1e3 for k, v in modes.items()}
             line['gather_bytes_per_rank'] = shard.layout.nbytes
             line['gather_record'] = 'compact' if shard.compact else 'full'
@@ -961,7 +1015,7 @@ def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, sh
     flops = 4 * 256 * P + 5 * 256 * 2
     achieved_tf = flops * E / (kernel_ms * 1e-3) / 1e12
     peak_tf = F64_VALU_PEAK_TFLOPS if args.precision == 'f64' else 157.3
-    kernel = getattr(eng, 'many_kernel', eng.step_kernel) if shard is None else eng.step_kernel
+    kernel = getattr(eng, 'many_kernel', eng.step_kernel)
     persistent = kernel.startswith('optimize_lr_persist_kernel')
     # bytes a persistent launch of S steps moves per env-step: actions 4P and
     # the outputs 4(2P+1) + 17 every step, the state (W, W0, G read; W, G
@@ -981,10 +1035,16 @@ def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, sh
             'n_features': 10, 'n_classes': 2, 'batch_size': 256,
             'steps_per_launch': S if persistent else 1,
             'outputs': ('every step kept: a [%d]-record slab per launch' % S
-                        if persistent else 'every step into the same output buffers'),
+                        if persistent and shard is None else
+                        'every step kept: [%d]-record slots, all-gathered' % shard.chunk
+                        if shard is not None and shard.chunk > 1 else
+                        'every step into the same output buffers'),
             'parallelism': 'env-sharded x%d (no collective)' % world
-            if shard is None else 'env-sharded x%d + one RCCL all-gather of the packed '
-            'outputs per step, pipelined over 2 buffers' % world,
+            if shard is None else
+            ('env-sharded x%d; chunks of %d steps: one persistent launch, then ONE RCCL '
+             'all-gather of the %d compact records, pipelined over 2 slots' % (
+                 world, shard.chunk, shard.chunk) if shard.chunk > 1 else
+             'env-sharded x%d + one RCCL all-gather of the packed outputs per step' % world),
         },
         'roofline': {
             'bound': 'mfma', 'pipe': 'f64 (MFMA + VALU, one 78.6 TF/s rate on gfx950)',

@@ -10,6 +10,13 @@ packed byte buffer (one aligned segment per field, no packing kernels) and
 ``all_gather_into_tensor`` concatenates the ranks' buffers -- RCCL over xGMI
 under the ``nccl`` backend, gloo in the CPU tests.
 
+The chunk schedule (``chunk`` = K > 1): the engine runs K steps in ONE
+persistent launch (``rollout_device``) whose step t writes record t of a
+[K]-record buffer, and ONE collective gathers all K records
+(``gather_chunk``): the collective's fixed cost is paid once per K steps,
+and with two buffers (``slots=2``) the gather of chunk c runs on RCCL's
+stream while chunk c + 1's launch writes the other buffer.
+
 The reference has no multi-GPU code; its scaling unit is one worker per env
 (custom_envs/vectorize/concurrentvecenv.py:74-92).
 """
@@ -64,10 +71,13 @@ class PackedLayout:
             out[name] = buf[off:off + size].view(dtype).view((num_envs * rows,) + tail)
         return out
 
-    def rank_views(self, gathered, world):
+    def rank_views(self, gathered, world, rank_stride=None, offset=0):
         """Zero-copy views of an all-gathered buffer: field -> tensor of shape
         (world, capacity * rows, *tail), rank r's shard in row r (only its
-        first counts[r] * rows entries are live)."""
+        first counts[r] * rows entries are live).  ``rank_stride`` (bytes
+        between ranks' records; default one record) and ``offset`` (bytes to
+        this record in rank 0's part) address record t of a gathered chunk."""
+        rank_stride = self.nbytes if rank_stride is None else rank_stride
         out = {}
         for name, dtype, rows, tail in self.fields:
             size = torch.empty((), dtype=dtype).element_size()
@@ -76,7 +86,22 @@ class PackedLayout:
             inner = [1] * len(dims)
             for i in range(len(dims) - 2, -1, -1):
                 inner[i] = inner[i + 1] * dims[i + 1]
-            out[name] = flat.as_strided((world,) + dims, (self.nbytes // size,) + tuple(inner),
+            out[name] = flat.as_strided((world,) + dims, (rank_stride // size,) + tuple(inner),
+                                        flat.storage_offset() + (offset + self.offsets[name]) // size)
+        return out
+
+    def chunk_views(self, buf, num_envs, k):
+        """Field -> (k, num_envs * rows, *tail) views of a [k]-record buffer
+        (record t at t * nbytes): the output slab of a k-step rollout."""
+        out = {}
+        for name, dtype, rows, tail in self.fields:
+            size = torch.empty((), dtype=dtype).element_size()
+            flat = buf.view(dtype)
+            dims = (num_envs * rows,) + tuple(tail)
+            inner = [1] * len(dims)
+            for i in range(len(dims) - 2, -1, -1):
+                inner[i] = inner[i + 1] * dims[i + 1]
+            out[name] = flat.as_strided((k,) + dims, (self.nbytes // size,) + tuple(inner),
                                         flat.storage_offset() + self.offsets[name] // size)
         return out
 
@@ -104,9 +129,9 @@ class GatheredOutputs(Mapping):
     ``snapshot()``, which materialises every field as its own tensor.
     """
 
-    def __init__(self, layout, gathered, counts, derived=None):
+    def __init__(self, layout, gathered, counts, derived=None, rank_stride=None, offset=0):
         self.layout, self.counts = layout, counts
-        self.rank_major = layout.rank_views(gathered, len(counts))
+        self.rank_major = layout.rank_views(gathered, len(counts), rank_stride, offset)
         self._rows = {name: r for name, _, r, _ in layout.fields}
         self._derived = dict(derived or {})
         self._flat = {}
@@ -148,14 +173,15 @@ class ShardedEnvs:
     """
 
     def __init__(self, engine, num_envs, rank=0, world=1, group=None, device=None, slots=1,
-                 collective=None, compact=None):
+                 collective=None, compact=None, chunk=1):
         """``collective``: run the all-gather even at world 1 (tests the RCCL
         path on one GPU); default: only when world > 1.  ``compact``: have the
         engine write (and the collective move) the compact record -- obs
         without its identically-zero weight block, done folded into
         episode_len -- when the engine offers it (``set_compact_outputs``);
         default: whenever the collective runs.  ``gather`` rebuilds the full
-        fields lazily."""
+        fields lazily.  ``chunk`` = K: every slot holds K step records
+        (``rollout``, ``gather_chunk``)."""
         self.engine, self.rank, self.world, self.group = engine, rank, world, group
         self.collective = world > 1 if collective is None else bool(collective)
         self.num_envs = int(num_envs)
@@ -182,13 +208,19 @@ class ShardedEnvs:
         # slot of the gathered buffer, so the all-gather moves only the other
         # ranks' records (NCCL/RCCL in-place form: send = recv + rank * count;
         # at world 1 it has nothing to move)
-        nb = self.layout.nbytes
+        self.chunk = int(chunk)
+        if self.chunk < 1:
+            raise ValueError('chunk must be >= 1')
+        nb = self.layout.nbytes * self.chunk
         self.gathered = [torch.zeros(world * nb, dtype=torch.uint8, device=device)
                          if self.collective else None for _ in range(slots)]
         self.buffers = [g[rank * nb:(rank + 1) * nb] if g is not None
                         else torch.zeros(nb, dtype=torch.uint8, device=device)
                         for g in self.gathered]
+        # record 0 of every slot: what the one-step calls write
         self.outs = [self.layout.views(b, engine.num_envs) for b in self.buffers]
+        # every record of every slot: what a K-step rollout writes
+        self.slabs = [self.layout.chunk_views(b, engine.num_envs, self.chunk) for b in self.buffers]
 
     @property
     def buffer(self):
@@ -214,12 +246,63 @@ class ShardedEnvs:
         self.engine.step_device(actions, self.outs[slot])
         return self.outs[slot]
 
+    def rollout(self, actions, slot=0, k=None):
+        """k (default: chunk) steps in one call of the engine's
+        ``rollout_device``: step t reads actions[t] and writes record t of
+        the slot."""
+        k = self.chunk if k is None else int(k)
+        if not 1 <= k <= self.chunk:
+            raise ValueError('rollout of %d steps into a %d-record slot' % (k, self.chunk))
+        self.engine.rollout_device(k, actions, self.slabs[slot], self.layout.nbytes)
+        return self.slabs[slot]
+
+    def rollout_runner(self, actions, slot=0, k=None):
+        """``rollout`` bound once (the engine's pre-bound form when it has one)."""
+        k = self.chunk if k is None else int(k)
+        if hasattr(self.engine, 'rollout_runner'):
+            return self.engine.rollout_runner(k, actions, self.slabs[slot], self.layout.nbytes)
+        return lambda: self.rollout(actions, slot, k)
+
+    def gather_chunk(self, slot=0, async_op=False, k=None):
+        """ONE collective for the k (default: chunk) records of a slot: every
+        rank gets every rank's k steps.  Returns a list of k
+        ``GatheredOutputs`` (step t's global outputs; views of the gathered
+        buffer, built lazily) and, with ``async_op``, the collective's work
+        handle.  A k below the chunk gathers the first k records
+        (out of place: the in-place form needs whole slots)."""
+        k = self.chunk if k is None else int(k)
+        nb = self.layout.nbytes
+        world = len(self.counts)
+        work = None
+        if not self.collective:
+            gathered, stride = self.buffers[slot], nb * self.chunk
+        else:
+            import torch.distributed as dist
+            if k == self.chunk:
+                gathered, stride = self.gathered[slot], nb * self.chunk
+                work = dist.all_gather_into_tensor(gathered, self.buffers[slot], group=self.group,
+                                                   async_op=async_op)
+            else:
+                gathered, stride = torch.empty(world * k * nb, dtype=torch.uint8,
+                                               device=self.buffers[slot].device), k * nb
+                work = dist.all_gather_into_tensor(gathered, self.buffers[slot][:k * nb],
+                                                   group=self.group, async_op=async_op)
+        counts = self.counts if self.collective else [self.hi - self.lo]
+        steps = [GatheredOutputs(self.layout, gathered, counts, self.derived, rank_stride=stride,
+                                 offset=t * nb) for t in range(k)]
+        return (steps, work) if async_op else steps
+
     def gather(self, slot=0, async_op=False):
         """Every rank gets the global outputs: ONE all_gather_into_tensor of the
         packed buffer.  Returns ``GatheredOutputs`` (at world 1 without the
         collective, views of this rank's own buffer); with ``async_op`` also the
         collective's work handle, whose ``wait()`` orders the caller's current
         stream after it."""
+        if self.chunk > 1:                  # record 0 of a chunk slot
+            steps, work = self.gather_chunk(slot, True, k=1)
+            if work is not None and not async_op:
+                work.wait()
+            return (steps[0], work) if async_op else steps[0]
         if not self.collective:
             res = GatheredOutputs(self.layout, self.buffers[slot], [self.hi - self.lo],
                                   self.derived)

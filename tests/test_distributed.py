@@ -75,6 +75,52 @@ class OracleShardEngine:
             out['accuracy'][i] = info['accuracy']
 
 
+    def rollout_device(self, k, actions, fields, record_bytes):
+        """k steps, step t's outputs into record t (the HIP engine's
+        ce_step_many_strided contract)."""
+        for t in range(k):
+            self.step_device(actions[t], {n: v[t] for n, v in fields.items()})
+
+
+def _chunk_rollout(features, targets, num_envs, rank, world, chunk, steps=44, compact=True):
+    """The chunk schedule: K-step rollouts into alternating slots, one
+    gather per chunk (the tail chunk shorter), every step's global outputs
+    snapshotted in order."""
+    lo, hi = shard_range(num_envs, world, rank)
+    shard = ShardedEnvs(OracleShardEngine(features, targets, hi - lo, compact), num_envs, rank,
+                        world, device='cpu', compact=compact, slots=2, chunk=chunk,
+                        collective=world > 1)
+    shard.seed(100)
+    shard.reset()
+    rec = [shard.gather().snapshot()]
+    acts = torch.from_numpy(np.random.RandomState(3).normal(
+        0, 0.01, (steps, num_envs, 20)).astype(np.float32))
+    t = c = 0
+    while t < steps:
+        k = min(chunk, steps - t)
+        slot = c % 2
+        shard.rollout(acts[t:t + k, lo:hi].contiguous(), slot, k)
+        rec += [g.snapshot() for g in shard.gather_chunk(slot, k=k)]
+        t += k
+        c += 1
+    return rec
+
+
+def _chunk_worker(rank, world, port, features, targets, expected, chunk):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        got = _chunk_rollout(features, targets, 5, rank, world, chunk)
+        assert len(got) == len(expected)
+        for t, (g, e) in enumerate(zip(got, expected)):
+            for key in e:
+                assert torch.equal(g[key], e[key]), (rank, t, key, chunk)
+    finally:
+        dist.destroy_process_group()
+
+
 def _rollout(features, targets, num_envs, rank, world, steps=44, compact=False):
     lo, hi = shard_range(num_envs, world, rank)
     shard = ShardedEnvs(OracleShardEngine(features, targets, hi - lo, compact), num_envs, rank,
@@ -289,3 +335,22 @@ def test_gloo_multiagent_gather_equals_single_rank(world):
     expected = _multi_rollout(5, 0, 1)
     assert any(bool(r['done'].any()) for r in expected)
     mp.spawn(_multi_worker, args=(world, _free_port(), expected), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize('chunk', [1, 7, 20])
+@pytest.mark.parametrize('world', [2, 3])
+def test_gloo_chunk_schedule_equals_single_rank(lr_dataset, world, chunk):
+    """The chunk schedule (one K-step rollout and ONE all-gather of its K
+    compact records per chunk, two alternating slots, a shorter tail chunk
+    gathered out of place): 5 envs over 2 and 3 ranks give, step for step,
+    the same global arrays as a 1-rank run of per-step gathers of the full
+    record, bit for bit (concurrentvecenv.py:99-104,200-227 reassembly)."""
+    import torch.multiprocessing as mp
+    features, targets = lr_dataset
+    expected = [{k: v.clone() for k, v in r.items()} for r in _rollout(features, targets, 5, 0, 1)]
+    one = _chunk_rollout(features, targets, 5, 0, 1, chunk)
+    for t, (g, e) in enumerate(zip(one, expected)):
+        for key in e:
+            assert torch.equal(g[key], e[key]), (t, key)
+    mp.spawn(_chunk_worker, args=(world, _free_port(), features, targets, expected, chunk),
+             nprocs=world, join=True)

@@ -235,14 +235,17 @@ def test_world_n_on_one_gpu_matches_world_1(tmp_path, world, compact, pipelined,
 def test_bench_n_ranks_rehearsal_on_one_gpu():
     """bench.py's N-rank path end to end on a 1-GPU box (--one-gpu-rehearsal:
     2 ranks on cuda:0, the collectives on gloo, so the gathers run eager):
-    launcher, shards, per-step gathers in both schedules, max-over-ranks
-    timing and rank 0's one JSON line, marked as a rehearsal."""
+    launcher, shards, the chunk schedule (persistent 4-step launches, one
+    gather per chunk, a shorter tail chunk) as `value`, the per-step gathers
+    in both schedules beside it, max-over-ranks timing and rank 0's one JSON
+    line, marked as a rehearsal."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--one-gpu-rehearsal',
-           '--steps', '5', '--warmup', '2', '--no-cpu-baseline', '--envs', '512']
+           '--steps', '10', '--warmup', '2', '--chunk-steps', '4', '--no-cpu-baseline',
+           '--no-measure-traffic', '--envs', '512']
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root)
     assert res.returncode == 0, res.stderr[-2000:]
     lines = [json.loads(l) for l in res.stdout.splitlines() if l.startswith('{')]
@@ -250,5 +253,8 @@ def test_bench_n_ranks_rehearsal_on_one_gpu():
     line = lines[0]
     assert line['n_gpus'] == 2 and 'rehearsal' in line
     assert line['config']['global_envs'] == 1024
-    assert line['value_gather_serial'] > 0 and line['value_gather_pipelined'] > 0
+    assert line['value_gather_serial_per_step'] > 0 and line['value_gather_pipelined_per_step'] > 0
+    assert line['gather_mode'] == 'chunk_pipelined' and line['gather_chunk_steps'] == 4
+    assert line['value_gather_chunk_serial'] > 0
+    assert line['value'] == line['value_gather_chunk_pipelined']
     assert line['gather_record'] == 'compact'

@@ -8,17 +8,30 @@ entry turns float32 summation-order noise into an arbitrary ratio:
   arithmetic in a different summation order:
     exact      done flags, episode lengths, the composed row order
                (reset + epoch-end shuffles), theta at every reset;
-    1e-4       theta and the newest gradient, relative to max |.| of the
-               env's vector; batch loss and reward relative;
-* formula parity on the engine's own state: every observation entry, the
-  loss ratio, and the info statistics recomputed in numpy from the engine's
-  theta / gradient / loss sequence with the reference's formulas
-  (multioptlrs.py:90-127), to float32 rounding of the float64 result;
-* observation parity with the live oracle's own rows, for the newest w~,
-  l~ and g~ entries: the state tolerance carried through each entry's ratio
-  (clipping to +-100 only shrinks a difference), on the entries whose
-  denominator is at least 1e-3 of the vector's max (at least a quarter of
-  them must qualify).
+    1e-5       theta and the newest gradient, relative to max |.| of the
+               env's vector (north_star's float32 bound); batch loss and
+               reward relative;
+* observation parity with the live oracle's own rows -- EVERY column: the
+  w~, l~ and g~ entries of all H ages (utils_env.py:155-161 over the
+  History rings, multioptlrs.py:90-103):
+    elementwise  each entry whose denominator is well conditioned (|den| >=
+                 1e-3 of its vector's max; at least a quarter qualify) within
+                 the engine's MEASURED state differences carried through the
+                 ratio, 2 (d_num + |r| d_den) / |den|, plus float32 rounding
+                 (clipping to +-100 only shrinks a difference);
+    per row      ||d||_inf / ||ref||_inf <= 1e-5 on the agent rows whose
+                 every denominator is within 10x of its vector's max and
+                 whose ||ref||_inf >= 0.5;
+* info parity with the oracle's info dict: batch_loss, weights_mean /
+  weights_sum, loss_mean and the terminal loss to 1e-5 relative;
+  actions_mean / actions_std (the same float32 learning rates) to 1e-6 /
+  1e-4; grads_mean / grads_sum / grad_diff within the measured gradient
+  difference; adjusted_loss within its propagated bound;
+* formula parity on the engine's own state, as extra checks: every
+  observation entry, the loss ratio and the info statistics recomputed in
+  numpy from the engine's theta / gradient / loss sequence with the
+  reference's formulas (multioptlrs.py:90-127), to float32 rounding of the
+  float64 result.
 """
 import numpy as np
 import pytest
@@ -78,30 +91,36 @@ def _oracle_rows(obs_o, names):
     return np.asarray(obs_o, np.float64)
 
 
-def _ratio_close(got, want, num, den, what, state_tol=1e-4):
-    """Observation entries clip(num / |den|) - 1 (float32) from the engine
-    vs the oracle's own.  The engine's num and den are within state_tol of
-    the vectors' max of the oracle's (the state checks), so an entry's ratio
-    is within state_tol (max|num| + |ratio| max|den|) / |den|; twice that,
-    on the entries with |den| >= 1e-3 max|den| (a quarter at least)."""
-    num = np.abs(np.asarray(num, np.float64))
+def _ratio_close(got, want, num, den, d_num, d_den, what):
+    """Observation entries clip(num / |den|) - 1 (float32) from the engine vs
+    the oracle's own, for one column (one age of w~ or g~, every agent).
+    num / den are the ORACLE's vectors; d_num / d_den the max |engine -
+    oracle| of the same vectors (measured): an entry's ratio r is then
+    within (d_num + |r| d_den) / |den| of the oracle's; twice that plus
+    float32 rounding, on the entries with |den| >= 1e-3 max|den| (a quarter
+    at least).  Returns the mask of rows with |den| >= 0.1 max|den|."""
     den = np.abs(np.asarray(den, np.float64))
     mask = den >= 1e-3 * den.max()
     assert mask.mean() >= 0.25, (what, mask.mean())
-    w = want[mask]
-    tol = 2 * state_tol * (num.max() + np.abs(w + 1) * den.max()) / den[mask] + 1e-6
+    w = want[mask].astype(np.float64)
+    r = np.abs(w + 1)
+    tol = 2 * (d_num + r * d_den) / den[mask] + 2.0 ** -22 * (r + 1) + 1e-7
     err = np.abs(got[mask].astype(np.float64) - w)
-    assert np.all(err <= tol), (what, float((err - tol).max()))
+    assert np.all(err <= tol), (what, float((err - tol).max()), float(err.max()))
+    return den >= 0.1 * den.max()
 
 
-def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state_tol=1e-4,
+def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state_tol=1e-5,
                stats=None):
     """acts_env: [T][P] actions in row order for env i.  stats (optional
-    dict) counts the adjusted_grad comparisons and how many were finite."""
+    dict) counts the adjusted_grad comparisons and how many were finite,
+    the obs entries compared with the oracle elementwise and the rows
+    compared by norm, and the worst row error seen."""
     if stats is None:
         stats = {}
-    stats.setdefault('adj_grad', 0)
-    stats.setdefault('adj_grad_finite', 0)
+    for key in ('adj_grad', 'adj_grad_finite', 'entries', 'rows'):
+        stats.setdefault(key, 0)
+    stats.setdefault('row_err_max', 0.0)
     P = rows.size
     agent_row = np.empty(P, np.int64)
     agent_row[rows] = np.arange(P)
@@ -113,12 +132,27 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
     assert np.array_equal(rec['state0']['theta'][i], th0)
     assert np.all(rec['obs0'][i] == -1.0)
     names = env.names
+
+    def snapshot(g_engine, l_engine, th_engine):
+        """The oracle's newest raw-history entry and the engine's distance
+        from it (max |d| per vector).  A reset entry's loss (and, after an
+        auto-reset, its gradient) is not among the engine's outputs: its
+        distance is the state bound (state_tol of the vector's max) until the
+        first step's loss ratio pins the loss (below)."""
+        th_o = np.asarray(env.history['weights'][0], np.float64).copy()
+        g_o = np.asarray(env.history['gradients'][0], np.float64).copy()
+        l_o = float(env.history['losses'][0])
+        d_g = (state_tol * np.abs(g_o).max() + 1e-7 if g_engine is None else
+               float(np.abs(np.asarray(g_engine, np.float64) - g_o).max()))
+        d_l = state_tol * abs(l_o) if l_engine is None else abs(float(l_engine) - l_o)
+        return {'th': th_o, 'g': g_o, 'l': l_o, 'd_g': d_g, 'd_l': d_l,
+                'd_th': float(np.abs(np.asarray(th_engine, np.float64) - th_o).max())}
+
+    snaps = [snapshot(rec['state0']['gprev'][i], None, th0)]
     theta_prev = th0.astype(np.float64)
     g_prev = None           # engine gradient of the previous step (None after a reset)
     l_prev = None
     ring = []               # engine's age-0 obs entries of earlier steps this episode
-    th_o_prev = th0.astype(np.float64)   # the oracle's theta and gradient before the step
-    g_o_prev = None
     for t in range(acts_env.shape[0]):
         step = rec['steps'][t]
         act_rows = acts_env[t]
@@ -143,6 +177,25 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
         np.testing.assert_allclose(g_e, g_o, rtol=0, atol=state_tol * np.abs(g_o).max() + 1e-7)
         assert loss == pytest.approx(float(info_o['batch_loss']), rel=state_tol)
         assert step['reward'][i, 0] == pytest.approx(float(rew_o), rel=state_tol, abs=state_tol)
+        # ---- info parity with the oracle's info (multioptlrs.py:112-127)
+        info_e = step['info'][i]
+        d_g = float(np.abs(np.asarray(g_e, np.float64) - np.asarray(g_o, np.float64)).max())
+        assert float(info_e[2]) == pytest.approx(float(info_o['weights_mean']), rel=state_tol)
+        assert float(info_e[3]) == pytest.approx(float(info_o['weights_sum']), rel=state_tol)
+        assert float(info_e[4]) == pytest.approx(float(info_o['actions_mean']), rel=1e-6)
+        assert float(info_e[5]) == pytest.approx(float(info_o['actions_std']), rel=1e-4, abs=1e-9)
+        assert float(info_e[10]) == pytest.approx(float(info_o['loss_mean']), rel=state_tol)
+        # the ring's 5 gradients are each within the measured difference of
+        # the oracle's (the newest is d_g; older ones were checked as newest)
+        d_ring = max([d_g] + [sn['d_g'] for sn in snaps[-4:]])
+        assert abs(float(info_e[8]) - float(info_o['grads_mean'])) <= 2 * d_ring + 1e-6 * abs(
+            float(info_o['grads_mean'])) + 1e-12, t
+        assert abs(float(info_e[9]) - float(info_o['grads_sum'])) <= 2 * d_ring * 5 * P + 1e-6 * abs(
+            float(info_o['grads_sum'])) + 1e-9, t
+        assert abs(float(info_e[13]) - float(info_o['grad_diff'])) <= 2 * (d_g + snaps[-1]['d_g']) + \
+            1e-6 * float(info_o['grad_diff']) + 1e-12, t
+        if done_o and info_o['loss'] is not None:
+            assert float(info_e[0]) == pytest.approx(float(info_o['loss']), rel=state_tol)
         # ---- formula parity on the engine's own sequence
         obs = step['obs'][i][agent_row]            # agent order, [P][3H]
         if done_o:
@@ -152,15 +205,47 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
             env.reset()
             assert np.array_equal(st['order'][i], env.order()), t
             theta_prev, g_prev, l_prev, ring = th0.astype(np.float64), None, None, []
-            th_o_prev, g_o_prev = th0.astype(np.float64), None
+            snaps = [snapshot(None, None, th0)]
             continue
-        # ---- observation parity with the oracle's rows (well-conditioned entries)
+        snaps.append(snapshot(g_e, loss, theta_after))
+        if len(snaps) == 2:
+            # the reset loss through the engine's first loss ratio
+            # (info adjusted_loss = float32(l_1 / |l_0|)): l_0 = l_1 / ratio
+            ratio_e = float(step['info'][i, 11])
+            if ratio_e != 0 and np.isfinite(ratio_e):
+                l0_e = abs(loss / ratio_e)
+                snaps[0]['d_l'] = abs(l0_e - abs(snaps[0]['l'])) + 2.0 ** -22 * abs(snaps[0]['l'])
+        # ---- observation parity with the oracle's rows: every column, every age
         rows_o = _oracle_rows(obs_o, names)
-        _ratio_close(obs[:, 0], rows_o[:, 0], th_o, th_o_prev, ('w', t))
-        if g_o_prev is not None:
-            _ratio_close(obs[:, 2 * H], rows_o[:, 2 * H], g_o, g_o_prev, ('g', t))
-        assert float(obs[0, H]) == pytest.approx(float(rows_o[0, H]), rel=1e-3, abs=1e-3)
-        th_o_prev, g_o_prev = np.asarray(th_o, np.float64).copy(), np.asarray(g_o, np.float64).copy()
+        well = np.ones(P, bool)
+        n_age = len(snaps) - 1                   # ages with a ratio this episode
+        for k in range(H):
+            if k >= n_age:                       # zero-initialised ring: exactly -1
+                for col in (k, H + k, 2 * H + k):
+                    assert np.all(obs[:, col] == -1.0) and np.all(rows_o[:, col] == -1.0), (t, col)
+                continue
+            new, old = snaps[-1 - k], snaps[-2 - k]
+            well &= _ratio_close(obs[:, k], rows_o[:, k], new['th'], old['th'], new['d_th'],
+                                 old['d_th'], ('w', t, k))
+            well &= _ratio_close(obs[:, 2 * H + k], rows_o[:, 2 * H + k], new['g'], old['g'],
+                                 new['d_g'], old['d_g'], ('g', t, k))
+            r = abs(float(rows_o[0, H + k]) + 1)
+            tol_l = 2 * (new['d_l'] + r * old['d_l']) / abs(old['l']) + 2.0 ** -22 * (r + 1) + 1e-7
+            assert np.all(np.abs(obs[:, H + k].astype(np.float64) - rows_o[:, H + k]) <= tol_l), \
+                ('l', t, k)
+            stats['entries'] += 2 * P + 1
+        ref_inf = np.abs(rows_o).max(axis=1)
+        sel = well & (ref_inf >= 0.5)
+        if sel.any():
+            row_err = np.abs(obs[sel].astype(np.float64) - rows_o[sel]).max(axis=1) / ref_inf[sel]
+            stats['rows'] += int(sel.sum())
+            stats['row_err_max'] = max(stats['row_err_max'], float(row_err.max()))
+            assert row_err.max() <= 1e-5, (t, float(row_err.max()))
+        # adjusted_loss (info) against the oracle's, within the l~ bound
+        r = abs(float(info_o['adjusted_loss']))
+        assert abs(float(info_e[11]) - float(info_o['adjusted_loss'])) <= 2 * (
+            snaps[-1]['d_l'] + r * snaps[-2]['d_l']) / abs(snaps[-2]['l']) + 2.0 ** -22 * (r + 1) + 1e-7
+        # extra: the engine's own sequence through the reference's formulas
         w_new = _obs_form(_ratio(theta_after, theta_prev))
         assert np.array_equal(obs[:, 0], w_new), t
         if g_prev is not None:
@@ -183,16 +268,12 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
             assert np.array_equal(obs[:, k], old[:, 0]), (t, k)
             assert np.array_equal(obs[:, 2 * H + k], old[:, 2 * H]), (t, k)
             assert np.all(obs[:, H + k] == old[0, H])
-        for k in range(len(ring) + 1, H):
-            assert np.all(obs[:, k] == -1.0) and np.all(obs[:, 2 * H + k] == -1.0)
         wsum = np.abs(theta_after).sum()
         assert float(step['info'][i, 3]) == pytest.approx(wsum, rel=1e-6)
         lr = (10.0 ** (act_rows[agent_row].astype(np.float32) - np.float32(4)).astype(np.float64)
               ).astype(np.float32).astype(np.float64)
         assert float(step['info'][i, 4]) == pytest.approx(lr.mean(), rel=1e-6)
         assert float(step['info'][i, 5]) == pytest.approx(lr.std(), rel=1e-4, abs=1e-9)
-        assert float(step['info'][i, 10]) == pytest.approx(float(info_o['loss_mean']),
-                                                           rel=state_tol)
         ring.append(obs.copy())
         theta_prev, g_prev, l_prev = theta_after, g_e.astype(np.float64), loss
 

@@ -139,3 +139,26 @@ def test_unsupported_mlp_shape_is_loud(change):
     handle = ctypes.c_void_p()
     assert lib.ce_create(ctypes.byref(cfg), x.ctypes.data, y.ctypes.data,
                          ctypes.byref(handle)) == _native.CE_EUNSUPPORTED
+
+
+def test_stale_hip_error_is_reported_not_lost():
+    """An entry point that finds a sticky HIP error left by another component
+    clears it (so it is not reported as its own failure) but keeps it:
+    ce_stale_error_count counts it, ce_stale_error_note names it, and the
+    Python side warns once per new batch.  Injected through the library's
+    test hook, exactly as CE_CLEAR_STALE_ERROR records one."""
+    import warnings
+    lib = _native.load()
+    lib.ce_test_note_stale_error.argtypes = [ctypes.c_int32]
+    before = lib.ce_stale_error_count()
+    _native.warn_stale()                       # absorb anything earlier in this process
+    assert lib.ce_test_note_stale_error(700) == _native.CE_OK
+    assert lib.ce_stale_error_count() == before + 1
+    note = lib.ce_stale_error_note().decode()
+    assert '700' in note and 'injected' in note and 'cleared' in note
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter('always')
+        assert _native.warn_stale() == before + 1
+        assert _native.warn_stale() == before + 1          # once, not on every call
+    msgs = [str(w.message) for w in caught if issubclass(w.category, RuntimeWarning)]
+    assert len(msgs) == 1 and '700' in msgs[0]
