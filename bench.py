@@ -614,7 +614,7 @@ def main():
     # consumes), written by ONE persistent launch per S steps where the
     # engine has the K-step kernel (ce_step_many_strided)
     slab = None
-    if args.workload == 'optimize' and shard is None and hasattr(eng, 'alloc_rollout'):
+    if args.workload in ('optimize', 'multi') and shard is None and getattr(eng, 'persistent', False):
         slab = eng.alloc_rollout(S)
         out = {k: v[0] for k, v in slab[0].items() if k != '_buffer'}
     eng.reset_device(out)
@@ -789,7 +789,7 @@ def main():
         primary(args.warmup)
         torch.cuda.synchronize()
         elapsed = _timed(torch, dist, primary, args.steps)
-        if slab is not None and getattr(eng, 'persistent', False):
+        if slab is not None:
             # the same steps as one launch per step (the one-step kernel,
             # what a closed-loop caller gets), timed the same way: the A/B
             # beside `value`
@@ -943,7 +943,7 @@ def _common(args, world, E, S, elapsed, shard):
 # and reported in roofline.traffic_source; --measure-traffic takes them in
 # the run instead.
 TRAFFIC_ROUND = 'r05'
-TRAFFIC_MARKER = {'optimize': 'optimize_lr_', 'multi': 'multi_step_kernel',
+TRAFFIC_MARKER = {'optimize': 'optimize_lr_', 'multi': 'multi_',
                   'mlp': 'mlp_step_kernel', 'net': 'net_finish_kernel',
                   'nn': 'nn_finalize_kernel', 'mnist': 'optimize_'}
 
@@ -957,7 +957,7 @@ def _traffic_name(args, eng):
 def _traffic_steps(args):
     """Steps per counted dispatch: the bench's launch size for the persistent
     K-step kernel (every dispatch the same S steps), else 1."""
-    if args.workload == 'optimize' and int(os.environ.get('CE_PERSIST', '1')) != 0:
+    if args.workload in ('optimize', 'multi') and int(os.environ.get('CE_PERSIST', '1')) != 0:
         return max(1, min(args.graph_steps, args.steps))
     return 1
 
@@ -1069,6 +1069,14 @@ def multi_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard
     P, H = eng.n_params, eng.max_history
     bpe = multi_bytes_per_env_step(P, H)
     achieved_gbs = bpe * E / (kernel_ms * 1e-3) / 1e9
+    kernel = getattr(eng, 'many_kernel', 'multi_step_kernel<4>')
+    persistent = kernel.startswith('multi_persist_kernel')
+    # a persistent launch of S steps moves per env-step the actions 4P and
+    # the outputs (obs 12HP, reward 4P, done P, info 56, length 4); the state
+    # (theta, g, the raw ring 5(1 + 2P), the adjusted ring H(1 + 2P) floats +
+    # HP doubles, step) is read and written once per launch
+    state = 4 * (2 * P + 5 * (1 + 2 * P) + H * (1 + 2 * P)) + 8 * H * P + 4
+    moved = (4 * P + 12 * H * P + 4 * P + P + 56 + 4 + 2 * state / S) if persistent else bpe
     line = {'metric': METRIC_MULTI}
     line.update(_common(args, world, E, S, elapsed, shard))
     line.update({
@@ -1081,6 +1089,7 @@ def multi_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard
                         '%d envs (%d agent rows) per GPU, in-kernel auto-reset, '
                         'device-resident actions/outputs' % (E, E * P),
             'envs_per_gpu': E, 'global_envs': world * E, 'agents': P, 'max_history': H,
+            'steps_per_launch': S if persistent else 1,
             'graph_steps': S, 'parallelism': 'env-sharded x%d (no collective)' % world
             if shard is None else 'env-sharded x%d + one RCCL all-gather of the packed '
             'outputs per step, pipelined over 2 buffers' % world,
@@ -1090,8 +1099,10 @@ def multi_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard
             'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
             'traffic': None,
             'bytes_per_env_step': bpe, 'kernel_ms_median': kernel_ms,
-            'kernel_ms_mean': kernel_ms_mean,
-            'kernel': 'ce::multi_step_kernel<4>',
+            'kernel_ms_mean': kernel_ms_mean, 'bytes_per_env_step_moved': moved,
+            'kernel': 'ce::' + kernel, 'steps_per_launch': S if persistent else 1,
+            'note': 'bytes_per_env_step: the state read and written every step (DESIGN 3.6); '
+                    'bytes_per_env_step_moved: what the launch form moves',
         },
     })
     return line

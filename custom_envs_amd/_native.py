@@ -35,7 +35,8 @@ EXPORTS = (
     'ce_get_state', 'ce_set_state',
     'ce_multi_create', 'ce_multi_destroy', 'ce_multi_set_stream', 'ce_multi_reset',
     'ce_multi_step', 'ce_multi_step_async', 'ce_multi_wait', 'ce_multi_step_many',
-    'ce_multi_step_many_prepare',
+    'ce_multi_step_many_prepare', 'ce_multi_step_many_strided', 'ce_multi_set_persistent',
+    'ce_multi_step_many_kernel',
     'ce_multi_host_outputs', 'ce_multi_get_state',
     'ce_nn_create', 'ce_nn_destroy', 'ce_nn_set_stream', 'ce_nn_n_params', 'ce_nn_seed',
     'ce_nn_seed_draws', 'ce_nn_reset', 'ce_nn_step', 'ce_nn_step_async', 'ce_nn_wait',
@@ -137,6 +138,10 @@ def _declare(lib):
         'ce_multi_step_many': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
         'ce_multi_step_many_prepare': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs)],
                                        ctypes.c_int),
+        'ce_multi_step_many_strided': ([vp, i32, vp, i64, ctypes.POINTER(CeMultiOutputs), i64],
+                                       ctypes.c_int),
+        'ce_multi_set_persistent': ([vp, i32], ctypes.c_int),
+        'ce_multi_step_many_kernel': ([vp], ctypes.c_char_p),
         'ce_multi_host_outputs': ([vp, ctypes.POINTER(CeMultiOutputs)], ctypes.c_int),
         'ce_multi_get_state': ([vp, vp, vp], ctypes.c_int),
         'ce_nn_create': ([ctypes.POINTER(CeNnConfig), vp, vp, ctypes.POINTER(vp)], ctypes.c_int),

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -42,20 +43,32 @@ void launch_multi_step(const ce::MultiArgs &a, int, hipStream_t s) {
         hipLaunchKernelGGL((ce::multi_step_kernel<P, 0>), dim3(multi_grid<P>(a.E)),
                            dim3(ce::kMultiBlock), lds, s, a);
 }
+// K steps in one launch (multi_persist_kernel): the reference default history
+// H = 5 only (the compile-time instance the kernel needs)
+template <int P>
+void launch_multi_persist(const ce::MultiArgs &a, int k, long long act_stride, long long out_step,
+                          hipStream_t s) {
+    const size_t lds = ce::kMultiBlock / 64 * (64 / ce::Group<P>::G) * P * 3 * 5 * sizeof(float);
+    hipLaunchKernelGGL((ce::multi_persist_kernel<P, 5>), dim3(multi_grid<P>(a.E)), dim3(ce::kMultiBlock),
+                       lds, s, a, k, act_stride, out_step);
+}
 template <int P>
 void launch_multi_reset(const ce::MultiArgs &a, int, hipStream_t s) {
     hipLaunchKernelGGL(ce::multi_reset_kernel<P>, dim3(multi_grid<P>(a.E)),
                        dim3(ce::kMultiBlock), 0, s, a);
 }
 
+using MultiPersistFn = void (*)(const ce::MultiArgs &, int, long long, long long, hipStream_t);
+
 struct MultiEntry {
     int P;
     MultiFn step, reset;
+    MultiPersistFn persist;
 };
 
 // every even dimension count up to CE_MULTI_MAX_PARAMS (one lane per agent:
 // an env's agents are a group of 2..64 lanes of one wave)
-#define CE_MULTI_ENTRY(P) {P, launch_multi_step<P>, launch_multi_reset<P>},
+#define CE_MULTI_ENTRY(P) {P, launch_multi_step<P>, launch_multi_reset<P>, launch_multi_persist<P>},
 #define CE_MULTI_ENTRY8(P) CE_MULTI_ENTRY(P) CE_MULTI_ENTRY(P + 2) CE_MULTI_ENTRY(P + 4) CE_MULTI_ENTRY(P + 6)
 const MultiEntry kMulti[] = {CE_MULTI_ENTRY8(2) CE_MULTI_ENTRY8(10) CE_MULTI_ENTRY8(18)
                                  CE_MULTI_ENTRY8(26) CE_MULTI_ENTRY8(34) CE_MULTI_ENTRY8(42)
@@ -78,6 +91,10 @@ struct ce_multi_engine {
     char *d_out = nullptr, *h_out = nullptr;
     bool was_reset = false;
     ce::GraphCache graphs;   // ce_multi_step_many
+    // the K-step launch (multi_persist_kernel): max_history == 5, and chosen
+    // (ce_multi_set_persistent; CE_PERSIST=0 at create turns it off)
+    bool persist = false, persist_on = true;
+    std::string many_name, step_name;
 };
 
 namespace {
@@ -202,6 +219,11 @@ int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out) {
     if (!e) return fail(CE_ENOMEM, "ce_multi_create: host allocation failed");
     e->cfg = *cfg;
     e->kern = kern;
+    e->persist = cfg->max_history == 5;
+    if (const char *pe = std::getenv("CE_PERSIST")) e->persist_on = pe[0] != '0';
+    e->step_name = "multi_step_kernel<" + std::to_string(cfg->n_params) + "," +
+                   std::to_string(cfg->max_history == 5 ? 5 : 0) + ">";
+    e->many_name = "multi_persist_kernel<" + std::to_string(cfg->n_params) + ",5>";
     auto bail = [&](int code) {
         ce_multi_destroy(e);
         return code;
@@ -330,8 +352,30 @@ int multi_graph(ce_multi_engine *e, int32_t k, const float *actions, int64_t str
 
 }  // namespace
 
+namespace {
+
+int multi_many_ok(const ce_multi_engine *e, int32_t k, const float *actions, int64_t stride,
+                  const ce_multi_outputs *out) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    if (!e->was_reset) return fail(CE_ESTATE, "step_many() before the first reset()");
+    if (k <= 0 || !actions || stride < 0) return fail(CE_EINVAL, "bad arguments");
+    if (out && !complete(out)) return fail(CE_EINVAL, "device outputs must all be set");
+    return CE_OK;
+}
+
+}  // namespace
+
 int ce_multi_step_many(ce_multi_engine *e, int32_t k, const float *actions, int64_t stride,
                        const ce_multi_outputs *out) {
+    if (e && e->persist && e->persist_on) {
+        const int rc = multi_many_ok(e, k, actions, stride, out);
+        if (rc != CE_OK) return rc;
+        CE_CLEAR_STALE_ERROR();
+        const ce_multi_outputs o = out ? *out : region(e, e->d_out);
+        e->kern->persist(make_args(e, actions, o), k, stride, 0, e->stream);
+        CE_HIP(hipGetLastError());
+        return CE_OK;
+    }
     hipGraphExec_t exec;
     const int rc = multi_graph(e, k, actions, stride, out, &exec);
     if (rc != CE_OK) return rc;
@@ -341,8 +385,47 @@ int ce_multi_step_many(ce_multi_engine *e, int32_t k, const float *actions, int6
 
 int ce_multi_step_many_prepare(ce_multi_engine *e, int32_t k, const float *actions,
                                int64_t stride, const ce_multi_outputs *out) {
+    if (e && e->persist && e->persist_on) return multi_many_ok(e, k, actions, stride, out);
     hipGraphExec_t exec;
     return multi_graph(e, k, actions, stride, out, &exec);
+}
+
+int ce_multi_step_many_strided(ce_multi_engine *e, int32_t k, const float *actions, int64_t stride,
+                               const ce_multi_outputs *out, int64_t out_step) {
+    int rc = multi_many_ok(e, k, actions, stride, out);
+    if (rc != CE_OK) return rc;
+    if (!out) return fail(CE_EINVAL, "ce_multi_step_many_strided: needs caller output buffers");
+    if (out_step < 0 || out_step % 16 != 0)
+        return fail(CE_EINVAL, "ce_multi_step_many_strided: out_step_bytes must be a non-negative "
+                               "multiple of 16");
+    CE_CLEAR_STALE_ERROR();
+    if (e->persist && e->persist_on) {
+        e->kern->persist(make_args(e, actions, *out), k, stride, out_step, e->stream);
+    } else {
+        for (int s = 0; s < k; ++s) {
+            ce_multi_outputs o = *out;
+            const int64_t b = s * out_step;
+            o.obs = reinterpret_cast<float *>(reinterpret_cast<char *>(o.obs) + b);
+            o.reward = reinterpret_cast<float *>(reinterpret_cast<char *>(o.reward) + b);
+            o.done = o.done + b;
+            o.info = reinterpret_cast<float *>(reinterpret_cast<char *>(o.info) + b);
+            o.episode_len = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(o.episode_len) + b);
+            e->kern->step(make_args(e, actions + s * stride, o), grid_of(e), e->stream);
+        }
+    }
+    CE_HIP(hipGetLastError());
+    return CE_OK;
+}
+
+int ce_multi_set_persistent(ce_multi_engine *e, int32_t on) {
+    if (!e) return fail(CE_EINVAL, "null engine");
+    e->persist_on = on != 0;
+    return CE_OK;
+}
+
+const char *ce_multi_step_many_kernel(const ce_multi_engine *e) {
+    if (!e) return "";
+    return (e->persist && e->persist_on ? e->many_name : e->step_name).c_str();
 }
 
 int ce_multi_host_outputs(ce_multi_engine *e, ce_multi_outputs *view) {

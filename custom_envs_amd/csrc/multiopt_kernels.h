@@ -483,3 +483,268 @@ __global__ __launch_bounds__(kMultiBlock) void multi_step_kernel(MultiArgs a) {
 }
 
 }  // namespace ce
+
+namespace ce {
+
+// ---------------------------------------------------------------------------
+// K consecutive MultiOptLRs-v0 steps in ONE launch (the reference default
+// history HC = 5): ce_multi_step_many_strided / ce_multi_step_many.
+//
+// An env's whole state -- theta, the gradient, the 5-entry raw ring (loss,
+// g, w) and the H-entry adjusted ring in observation form with its |.| sums
+// -- is a few dozen values per lane: it is loaded once, lives in VGPRs for
+// the K steps (ring slots indexed by the same physical positions
+// multi_step_kernel uses, so every sum runs in the same order) and is stored
+// once.  Per step a wave reads only its actions (prefetched a step ahead)
+// and writes only the step's outputs into output record t (out_step bytes
+// apart; 0 = every step into the same record), so the launch floor, the
+// state round trip and the ring traffic of K one-step launches are paid
+// once.  The arithmetic is multi_step_kernel's, operation for operation
+// (tests/test_gpu_multi.py checks the bits against it).
+template <int P, int HC>
+__global__ __launch_bounds__(kMultiBlock) void multi_persist_kernel(MultiArgs a, int K, long long act_stride,
+                                                                   long long out_step) {
+#pragma clang fp contract(off)
+    constexpr int G = Group<P>::G;
+    constexpr int H = HC;
+    constexpr int row = 3 * H;
+    static_assert(HC > 0 && HC <= kMultiStageH, "compile-time history");
+    extern __shared__ float4 stage4[];
+    float *stage = reinterpret_cast<float *>(stage4);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t gt = static_cast<size_t>(blockIdx.x) * kMultiBlock + threadIdx.x;
+    const size_t e = gt / G;
+    const int i = static_cast<int>(gt % G);
+    const size_t E = a.E;
+    const bool env_ok = e < E;
+    const bool on = env_ok && i < P;
+    const size_t ec = env_ok ? e : 0;
+    const int ic = i < P ? i : 0;
+    const int r = P <= 10 ? ic : a.agent_row[ic];
+    const unsigned Eu = static_cast<unsigned>(E), eu = static_cast<unsigned>(ec);
+    const unsigned ep = eu * P + ic;
+
+    // ---- the state, once
+    int s_prev = at32(a.step, eu);
+    float act = at32(a.act, eu * P + r);
+    const float th_init = i < P ? a.init[i] : 0.0f;
+    const float g_init = i < P ? a.init_g[i] : 0.0f, l_init = a.init_l;
+    float th = at32(a.theta, ep);
+    float gc = at32(a.grad, ep);
+    float hl_v[kRawHist], hg_v[kRawHist], hw_v[kRawHist];
+#pragma unroll
+    for (int k = 0; k < kRawHist; ++k) {
+        hl_v[k] = at32(a.hl, k * Eu + eu);
+        hg_v[k] = at32(a.hg, k * Eu * P + ep);
+        hw_v[k] = at32(a.hw, k * Eu * P + ep);
+    }
+    float ol_v[H], og_v[H], ow_v[H];
+    double sa_v[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        ol_v[j] = at32(a.ol, j * Eu + eu);
+        og_v[j] = at32(a.og, j * Eu * P + ep);
+        ow_v[j] = at32(a.ow, j * Eu * P + ep);
+        sa_v[j] = at32(a.sa, j * Eu * P + ep);
+    }
+    const int span = 64 / G * P * row;       // floats of one wave's env block
+    float *lds = stage + wave * span;
+    float *const lrow = lds + ((lane / G) * P + r) * row;
+    const size_t e_first = (static_cast<size_t>(blockIdx.x) * kMultiBlock + wave * 64) / G;
+    const size_t envs = e_first < E ? (E - e_first < static_cast<size_t>(64 / G) ? E - e_first
+                                                                                  : static_cast<size_t>(64 / G))
+                                    : 0;
+    const int nblk = static_cast<int>(envs) * P * row;
+
+    for (int t = 0; t < K; ++t) {
+        // step t + 1's action, consumed at the end of this step
+        const float act_next = at32(a.act + (t + 1 < K ? (t + 1) * act_stride : 0), eu * P + r);
+        const long long ro = t * out_step;     // this step's output record, bytes past record 0
+        const int s = s_prev + 1;
+        // ---- update (multioptlrs.py:81-87), lr = 10^(a - 4)
+        const float x = act - 4.0f;
+        const float lr = static_cast<float>(exp10(static_cast<double>(x)));
+        const float thn = th - gc * lr;
+        float g, loss;
+        rosenbrock_lane<P>(thn, i, g, loss);
+        // ---- raw history append, observation v3 against the previous entry
+        const int slot = s % kRawHist, prev = (s - 1) % kRawHist;
+        double l_prev = 0.0;
+        float gp = 0.0f, wp = 0.0f;
+        double lsum = loss, gsum = g;
+#pragma unroll
+        for (int k = 0; k < kRawHist; ++k) {
+            if (k == prev) {
+                l_prev = hl_v[k];
+                gp = hg_v[k];
+                wp = hw_v[k];
+            }
+            if (k != slot) {
+                lsum += hl_v[k];
+                gsum += hg_v[k];
+            }
+        }
+        const double adj_l = ratio_fast(loss, static_cast<float>(l_prev));
+        const double adj_g = ratio_fast(g, gp);
+        const double adj_w = ratio_fast(thn, wp);
+        const float nw = static_cast<float>(clip100(adj_w) - 1.0);
+        const float nl = static_cast<float>(clip100(adj_l) - 1.0);
+        const float ng = static_cast<float>(clip100(adj_g) - 1.0);
+        const double nsum = fabs(adj_w) + fabs(adj_g) + fabs(adj_l);
+        const int aslot = (s - 1) % H;
+        // ---- reward v6 + termination (multioptlrs.py:102-107)
+        double reward = 1.0 - adj_l;
+        reward = reward < -100.0 ? -100.0 : (reward > 100.0 ? 100.0 : reward);
+        bool terminal = s >= a.max_batches;
+        if (!terminal && loss > 1e4f) {
+            terminal = true;
+            reward -= static_cast<double>(a.max_batches - s);
+        }
+        const bool wipe = terminal && a.auto_reset;
+        // ---- observation row: [w~ (H, newest first) | l~ (H) | g~ (H)]
+        double st_abs = 0.0;
+        const int k0 = aslot;
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            const int kk = k0 - j >= 0 ? k0 - j : k0 - j + H;
+            float wk = ow_v[j], gk = og_v[j], lk = ol_v[j];
+            double sk = sa_v[j];
+            if (kk == 0) {
+                wk = nw;
+                gk = ng;
+                lk = nl;
+                sk = nsum;
+            }
+            st_abs += sk;
+            if (on) {
+                lrow[kk] = wipe ? -1.0f : wk;
+                lrow[H + kk] = wipe ? -1.0f : lk;
+                lrow[2 * H + kk] = wipe ? -1.0f : gk;
+            }
+        }
+        // the ring entries of this step, in registers
+#pragma unroll
+        for (int k = 0; k < kRawHist; ++k)
+            if (k == slot) {
+                hg_v[k] = g;
+                hw_v[k] = thn;
+                hl_v[k] = loss;
+            }
+#pragma unroll
+        for (int j = 0; j < H; ++j)
+            if (j == aslot) {
+                og_v[j] = ng;
+                ow_v[j] = nw;
+                sa_v[j] = nsum;
+                ol_v[j] = nl;
+            }
+        // the wave's staged rows -> record t (one wave per workgroup: the LDS
+        // block is the wave's own, in-order within the wave)
+        __builtin_amdgcn_wave_barrier();
+        {
+            float *out = reinterpret_cast<float *>(reinterpret_cast<char *>(a.obs) + ro) + e_first * P * row;
+            constexpr int kV = (64 / G * P * 3 * HC / 4 + 63) / 64;
+            if ((nblk & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+                const float4 *src = reinterpret_cast<const float4 *>(lds);
+                float4 *dst4 = reinterpret_cast<float4 *>(out);
+                const int n4 = nblk >> 2;
+                float4 v[kV];
+#pragma unroll
+                for (int u = 0; u < kV; ++u) {
+                    const int q = lane + 64 * u;
+                    v[u] = src[q < n4 ? q : n4 - 1];
+                }
+#pragma unroll
+                for (int u = 0; u < kV; ++u) {
+                    const int q = lane + 64 * u;
+                    if (q < n4) dst4[q] = v[u];
+                }
+            } else {
+                for (int q = lane; q < nblk; q += 64) out[q] = lds[q];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // ---- info (multioptlrs.py:112-127), float64 group reductions.  An
+        // idle lane (agent i >= P of a group) carries its own values across
+        // the K steps, which may overflow: it contributes by a select, not by
+        // multiplying with 0 (the one-step kernel's `mine *`, identical for
+        // every finite value)
+        auto mine = [&](double v) { return on ? v : 0.0; };
+        const double wsum = group_sum<G>(mine(fabs(static_cast<double>(thn))));
+        const double amean = group_sum<G>(mine(static_cast<double>(lr))) / P;
+        const double dev = static_cast<double>(lr) - amean;
+        const double avar = group_sum<G>(mine(dev * dev)) / P;
+        const double adjg = group_sum<G>(mine(fabs(adj_g))) / P;
+        const double gdiff = group_sum<G>(mine(fabs(static_cast<double>(g) - static_cast<double>(gp)))) / P;
+        const double gsum_all = group_sum<G>(mine(gsum));
+        const double st_all = group_sum<G>(mine(st_abs));
+        if (on) {
+            if (i == 0) {
+                float *info = reinterpret_cast<float *>(reinterpret_cast<char *>(a.info) + ro) + eu * kMultiInfo;
+                info[0] = terminal ? loss : __builtin_nanf("");
+                info[1] = loss;
+                info[2] = static_cast<float>(wsum / P);
+                info[3] = static_cast<float>(wsum);
+                info[4] = static_cast<float>(amean);
+                info[5] = static_cast<float>(sqrt(avar));
+                info[6] = static_cast<float>(st_all / (P * row));
+                info[7] = static_cast<float>(st_all);
+                info[8] = static_cast<float>(gsum_all / (kRawHist * P));
+                info[9] = static_cast<float>(gsum_all);
+                info[10] = static_cast<float>(lsum / kRawHist);
+                info[11] = static_cast<float>(adj_l);
+                info[12] = static_cast<float>(adjg);
+                info[13] = static_cast<float>(gdiff);
+                at32(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro), eu) = s;
+            }
+            at32(reinterpret_cast<float *>(reinterpret_cast<char *>(a.reward) + ro), eu * P + r) =
+                static_cast<float>(reward);
+            at32(reinterpret_cast<uint8_t *>(a.done) + ro, eu * P + r) = terminal ? 1 : 0;
+        }
+        // ---- the next step's state: the auto-reset's (multi_store_reset) or this one
+        if (wipe) {
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k) {
+                hg_v[k] = k == 0 ? g_init : 0.0f;
+                hw_v[k] = k == 0 ? th_init : 0.0f;
+                hl_v[k] = k == 0 ? l_init : 0.0f;
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                og_v[j] = -1.0f;
+                ow_v[j] = -1.0f;
+                ol_v[j] = -1.0f;
+                sa_v[j] = 0.0;
+            }
+            th = th_init;
+            gc = g_init;
+            s_prev = 0;
+        } else {
+            th = thn;
+            gc = g;
+            s_prev = s;
+        }
+        act = act_next;
+    }
+    // ---- the state after K steps, once
+    if (on) {
+        at32(a.theta, ep) = th;
+        at32(a.grad, ep) = gc;
+#pragma unroll
+        for (int k = 0; k < kRawHist; ++k) {
+            at32(a.hg, k * Eu * P + ep) = hg_v[k];
+            at32(a.hw, k * Eu * P + ep) = hw_v[k];
+            if (i == 0) at32(a.hl, k * Eu + eu) = hl_v[k];
+        }
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            at32(a.og, j * Eu * P + ep) = og_v[j];
+            at32(a.ow, j * Eu * P + ep) = ow_v[j];
+            at32(a.sa, j * Eu * P + ep) = sa_v[j];
+            if (i == 0) at32(a.ol, j * Eu + eu) = ol_v[j];
+        }
+        if (i == 0) at32(a.step, eu) = s_prev;
+    }
+}
+
+}  // namespace ce

@@ -213,7 +213,12 @@ class OptimizeEngine:
 
     def derived_fields(self):
         """Fields the compact form leaves out, as functions of the fields it
-        stores (name -> fn(fields) -> tensor): the full obs rows and done."""
+        stores (name -> fn(fields) -> tensor): the full obs rows (zeros for
+        the wght_hist block), done (episode_len >= max_steps) and reward
+        (-objective).  The last is bit-exact because the compact form exists
+        only on the two-class full-batch kernel, where B == N makes the
+        minibatch loss and the full-data objective the same float64 number
+        (optimize.py:91,94-97) and float32(-x) == -float32(x)."""
         if not self.compact:
             return {}
         return compact_derived(self.act_dim, self.max_steps)

@@ -76,6 +76,55 @@ class MultiOptEngine:
         check(lib.ce_multi_create(ctypes.byref(cfg), ctypes.byref(handle)), 'ce_multi_create')
         self._lib, self._h, self._prefix = lib, handle, 'ce_multi_'
         self._bind_outputs()
+        self.many_kernel = lib.ce_multi_step_many_kernel(handle).decode()
+
+    # ------------------------------------------------- K steps in one launch
+    def set_persistent(self, on=True):
+        """K-step calls as ONE launch of multi_persist_kernel (max_history 5)
+        or one launch per step (on=False, the A/B form)."""
+        self._call('set_persistent', 1 if on else 0)
+        self.many_kernel = self._lib.ce_multi_step_many_kernel(self._h).decode()
+
+    @property
+    def persistent(self):
+        return self.many_kernel.startswith('multi_persist_kernel')
+
+    def alloc_rollout(self, k, torch_device=None):
+        """[k] output records (256-B aligned field segments per record):
+        (fields, record_bytes), fields[name] a (k, rows, ...) view."""
+        import torch
+        from custom_envs_amd.distributed import PackedLayout
+        lay = PackedLayout(self.output_fields(), self.num_envs)
+        buf = torch.zeros(int(k) * lay.nbytes, dtype=torch.uint8,
+                          device=torch_device or torch.device('cuda'))
+        fields = lay.chunk_views(buf, self.num_envs, int(k))
+        fields['_buffer'] = buf
+        return fields, lay.nbytes
+
+    def rollout_device(self, k, actions, fields, record_bytes, per_step_actions=True):
+        """k steps; step t reads actions[t] and writes record t of ``fields``
+        (ce_multi_step_many_strided)."""
+        if actions.numel() < (k if per_step_actions else 1) * self.rows or not actions.is_contiguous():
+            raise ValueError('actions must be a contiguous float32 tensor of k x E*P rows')
+        o = self._outputs({n: v[0] for n, v in fields.items() if n != '_buffer'})
+        stride = self.rows if per_step_actions else 0
+        self._call('step_many_strided', int(k), actions.data_ptr(), stride, ctypes.byref(o),
+                   int(record_bytes))
+
+    def rollout_runner(self, k, actions, fields, record_bytes, per_step_actions=True):
+        """rollout_device bound once."""
+        if actions.numel() < (k if per_step_actions else 1) * self.rows or not actions.is_contiguous():
+            raise ValueError('actions must be a contiguous float32 tensor of k x E*P rows')
+        o = self._outputs({n: v[0] for n, v in fields.items() if n != '_buffer'})
+        fn, h, ap, ref = self._fn('step_many_strided'), self._h, actions.data_ptr(), ctypes.byref(o)
+        kk, stride, rb = int(k), (self.rows if per_step_actions else 0), int(record_bytes)
+
+        def run():
+            rc = fn(h, kk, ap, stride, ref, rb)
+            if rc:
+                check(rc, self._prefix + 'step_many_strided')
+        run.keep = (actions, fields, o)
+        return run
 
     def _fn(self, name):
         return getattr(self._lib, self._prefix + name)
@@ -249,6 +298,16 @@ class NNMultiEngine(MultiOptEngine):
         self.n_params = int(lib.ce_nn_n_params(handle))
         self._bind_outputs()
         self.seed(seeds)
+        self.many_kernel = 'nn_* (one launch sequence per step)'
+
+    def set_persistent(self, on=True):
+        if on:
+            raise _native.NativeEngineError('the network problem has no K-step launch form')
+
+    def rollout_device(self, *args, **kwargs):
+        raise _native.NativeEngineError('the network problem has no strided K-step form')
+
+    rollout_runner = rollout_device
 
     @property
     def dims(self):

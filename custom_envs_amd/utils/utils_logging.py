@@ -149,7 +149,9 @@ class VecMonitor:
         self.data = [[] for _ in range(num_envs)]
         self.metric_history = [defaultdict(list) for _ in range(num_envs)]
         self.total_steps = np.zeros(num_envs, np.int64)
-        self.reset_info = {}
+        # per env, as each reference Monitor keeps its own current_reset_info
+        # (monitor.py:84-90): a partial reset stamps only the envs it resets
+        self.reset_info = [{} for _ in range(num_envs)]
 
     def reset(self, indices=None, **kwargs):
         idx = slice(None) if indices is None else indices
@@ -161,7 +163,11 @@ class VecMonitor:
         for key in self.reset_keywords:
             if kwargs.get(key) is None:
                 raise ValueError('Expected you to pass kwarg %s into reset' % key)
-            self.reset_info[key] = kwargs[key]
+        envs = range(len(self.reset_info)) if indices is None else np.arange(
+            len(self.reset_info))[indices]
+        for i in np.atleast_1d(envs):
+            for key in self.reset_keywords:
+                self.reset_info[int(i)][key] = kwargs[key]
         self.ep_reward[idx] = 0.0
         self.ep_len[idx] = 0
         self.current_episode[idx] += 1
@@ -197,7 +203,7 @@ class VecMonitor:
                 ep_info['episode'] = int(self.current_episode[i])
             for key in self.info_keywords:
                 ep_info[key] = info[key]
-            ep_info.update(self.reset_info)
+            ep_info.update(self.reset_info[i])
             self.data[i].append(ep_info)
             if len(self.data[i]) >= self.chunk_size:
                 _save_rows(self.paths[i], self.data[i])

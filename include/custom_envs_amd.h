@@ -49,7 +49,9 @@
  *                    -> OptEnvRunner.step         custom_envs/vectorize/optvecenv.py:38-46
  *                    -> MultiOptLRs.base_step     custom_envs/envs/multioptlrs.py:80-129
  *   ce_multi_step_async / ce_multi_wait / ce_multi_step_many(_prepare) / ce_multi_host_outputs /
- *   ce_multi_get_state / ce_multi_set_stream / ce_multi_destroy: as for Optimize-v0.
+ *   ce_multi_get_state / ce_multi_set_stream / ce_multi_destroy /
+ *   ce_multi_step_many_strided / ce_multi_set_persistent / ce_multi_step_many_kernel:
+ *                    as for Optimize-v0.
  *
  * MultiOptLRs-v0 over the neural-network problem (get_problem('nn')):
  *   ce_nn_create     MultiOptLRs.__init__(problem='nn')  multioptlrs.py:39-61
@@ -302,6 +304,16 @@ int ce_multi_step_many(ce_multi_engine *eng, int32_t k, const float *actions,
                        int64_t action_step_stride, const ce_multi_outputs *out);
 int ce_multi_step_many_prepare(ce_multi_engine *eng, int32_t k, const float *actions,
                                int64_t action_step_stride, const ce_multi_outputs *out);
+/* As ce_step_many_strided: step t writes every output advanced by
+ * t * out_step_bytes.  With max_history == 5 (the reference default,
+ * multioptlrs.py:39) the K steps are ONE launch of multi_persist_kernel (the
+ * state in registers across them); otherwise K step launches. */
+int ce_multi_step_many_strided(ce_multi_engine *eng, int32_t k, const float *actions,
+                               int64_t action_step_stride, const ce_multi_outputs *out,
+                               int64_t out_step_bytes);
+/* As ce_set_persistent / ce_step_many_kernel. */
+int ce_multi_set_persistent(ce_multi_engine *eng, int32_t on);
+const char *ce_multi_step_many_kernel(const ce_multi_engine *eng);
 int ce_multi_host_outputs(ce_multi_engine *eng, ce_multi_outputs *view);
 /* theta [E][P] (problem parameters in agent order) and current_step [E] */
 int ce_multi_get_state(ce_multi_engine *eng, float *theta, int32_t *step);

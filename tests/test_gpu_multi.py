@@ -361,3 +361,88 @@ def test_bad_config_is_rejected():
         MultiOptEngine(4, {'ndims': 3, 'initial_points': [0.0, 0.0, 0.0]})
     with pytest.raises(NativeEngineError):
         MultiOptEngine(0, 'func')
+
+
+def _multi_rollout(eng, acts, chunks):
+    """acts [T][E*P] through rollout_device calls of the given chunk sizes;
+    every step's outputs as numpy [T][...] and the final state."""
+    import torch
+    stream = torch.cuda.Stream()
+    rec = {}
+    with torch.cuda.stream(stream):
+        eng.set_stream(stream.cuda_stream)
+        eng.reset_device(eng.alloc_device_outputs())
+        dact = torch.from_numpy(acts).cuda()
+        t = 0
+        for k in chunks:
+            fields, rb = eng.alloc_rollout(k)
+            eng.rollout_device(k, dact[t:t + k].contiguous(), fields, rb)
+            stream.synchronize()
+            for name, v in fields.items():
+                if name != '_buffer':
+                    rec.setdefault(name, []).append(v.cpu().numpy())
+            t += k
+    return {k: np.concatenate(v) for k, v in rec.items()}, eng.get_state()
+
+
+@pytest.mark.parametrize('problem,E,MB,T,chunks', [
+    ('func4', 1024, 400, 45, [20, 20, 5]),      # config 5's shape; loss > 1e4 stops
+    ('func4', 77, 9, 40, [13, 1, 26]),           # max_batches ends, a partial last wave
+    ({'ndims': 6, 'initial_points': [-1.9, 2.0, -1.0, 1.5, 0.5, -0.5]}, 40, 12, 30, [30]),  # idle lanes
+])
+def test_persistent_multi_bit_equal_to_step_launches(problem, E, MB, T, chunks):
+    """multi_persist_kernel (K steps per launch, the state in registers) gives
+    the one-step kernel's bits for every output of every step and the final
+    theta / step: early stops (loss > 1e4), max_batches ends, a partial last
+    wave, and agent groups with idle lanes (P = 6 in groups of 8)."""
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    outs = []
+    for persist in (False, True):
+        eng = MultiOptEngine(E, problem, max_batches=MB, max_history=5)
+        eng.set_persistent(persist)
+        assert eng.persistent == persist
+        P = eng.n_params
+        acts = np.random.RandomState(E + MB).uniform(1.0, 3.0, (T, E * P)).astype(np.float32)
+        outs.append(_multi_rollout(eng, acts, chunks))
+        eng.close()
+    (a, sa), (b, sb) = outs
+    for name in a:
+        assert np.array_equal(a[name], b[name], equal_nan=True), name
+    assert any(a['done'].any(axis=1)), 'no episode ended'
+    for name in ('theta', 'step'):
+        assert np.array_equal(sa[name], sb[name]), name
+
+
+def test_persistent_multi_against_oracle():
+    """The persistent kernel against live oracle runners: 64 envs x 4 agents,
+    mixed stable / divergent action ranges, max_batches 30 over 70 steps in
+    launches of 25, 25, 20: every step's rows, reward, done, info."""
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    E, P, H, MB, T = 64, 4, 5, 30, 70
+    rs = np.random.RandomState(13)
+    lows = rs.uniform(-1.5, 1.5, E)
+    actions = np.stack([rs.uniform(lows[e], lows[e] + 1.5, (T, P)) for e in range(E)], 1)
+    actions = actions.astype(np.float32).reshape(T, E * P)
+    eng = MultiOptEngine(E, 'func4', max_batches=MB, max_history=H)
+    assert eng.many_kernel == 'multi_persist_kernel<4,5>'
+    got, st = _multi_rollout(eng, actions, [25, 25, 20])
+    eng.close()
+    refs = [OptEnvRunner(OracleMulti(P, max_batches=MB, max_history=H)) for _ in range(E)]
+    for r in refs:
+        r.reset()
+    for t in range(T):
+        for e, runner in enumerate(refs):
+            states, rewards, dones, infos = runner.step(list(actions[t, e * P:(e + 1) * P].reshape(P, 1)))
+            grad_abs = np.abs(runner._environment.history['gradients']).astype(np.float64)
+            if dones[0]:
+                states = runner.reset()
+            rows = slice(e * P, (e + 1) * P)
+            assert np.all(got['done'][t, rows] == dones[0]), (t, e)
+            assert int(got['episode_len'][t, e]) == infos[0]['episode']['l']
+            _close_rows(got['obs'][t, rows], np.stack(states))
+            assert abs(got['reward'][t, e * P] - rewards[0]) <= 1e-6 * max(1.0, abs(rewards[0]))
+            _close_info(got['info'][t, e], _ref_info(infos[0]), grad_abs=grad_abs)
+    for e, runner in enumerate(refs):
+        assert st['step'][e] == runner._environment.current_step
+        if st['step'][e]:
+            assert np.array_equal(st['theta'][e], runner._environment.model.params)
