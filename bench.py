@@ -1016,7 +1016,7 @@ def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, sh
     achieved_tf = flops * E / (kernel_ms * 1e-3) / 1e12
     peak_tf = F64_VALU_PEAK_TFLOPS if args.precision == 'f64' else 157.3
     kernel = getattr(eng, 'many_kernel', eng.step_kernel)
-    persistent = kernel.startswith('optimize_lr_persist_kernel')
+    persistent = kernel.startswith('optimize_lr_persist')
     # bytes a persistent launch of S steps moves per env-step: actions 4P and
     # the outputs 4(2P+1) + 17 every step, the state (W, W0, G read; W, G
     # written, f64; L, step r/w) once per launch

@@ -428,4 +428,372 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
 #endif
 }
 
+
+// The wave-specialised form: 4 ROW waves (one per SIMD, the row work of the
+// kernel above, tile for tile) and 4 EPILOGUE waves (the scalar / parameter
+// roles and the output stores) in one 512-thread workgroup.  Above, every
+// wave runs the epilogue after the step's barrier, so its dependent f64
+// chains (~0.6 us per step, the stamps of scripts/diag_persist.py) sit
+// between two steps' row work.  Here the row waves go straight from the
+// barrier into the next step's rows while the epilogue waves -- the younger,
+// lower-priority wave of each SIMD -- turn the partials of the step just
+// finished into its outputs, in the issue slots the row wave leaves; the
+// next barrier finds them done.  The LDS partials and staged observation
+// blocks are double-buffered by step parity, as above, so one barrier per
+// step orders both (row waves: rows t, partials t -> buf, barrier t;
+// epilogue waves: barrier t, flush obs t - 1, epilogue t from buf).  To fit
+// two waves per SIMD (256 registers each) the gradient A operands live in
+// the row wave's own LDS tiles instead of registers.  Same arithmetic, same summation
+// order as optimize_lr_persist_kernel<NKF, TPW, PAD, 4>: bit-identical.
+template <int NKF, int TPW, bool PAD>
+__global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<double> a, ManyArgs m) {
+    constexpr int W = 4;                                    // row waves
+    constexpr int BLK = 512;
+    constexpr int EB = BLK - kWave * W;                     // epilogue threads
+    constexpr int P_MAX = 2 * kLrMaxF;
+    constexpr int TD = lr_tile_doubles(NKF);
+    constexpr int PR = (kLrEnvs * P_MAX + EB - 1) / EB;
+    constexpr int OSM = 2 * P_MAX + 4;
+    constexpr int NG = TPW < 4 ? TPW : 4;
+    __shared__ double red_s[2][W][4][kWave];
+    __shared__ double red_l[2][W][kLrEnvs];
+    __shared__ double red_h[2][W][kLrEnvs];
+    __shared__ __attribute__((aligned(16))) float obs_s[2][kLrEnvs * OSM];
+    __shared__ double xgs[W][TPW][4][kWave];                // gradient A operands
+
+#ifdef CE_DIAG
+    unsigned long long lp_st[8] = {0};
+#endif
+    LP_STAMP(0);
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 15, h = lane >> 4;
+    const int E = a.E, F = a.F, P = 2 * F, N = a.N, B = a.B;
+    const int OS = a.obs_stride, OL = a.obs_lo;
+    const int e0 = blockIdx.x * kLrEnvs;
+    const double *img = reinterpret_cast<const double *>(a.data);
+    const int ntiles = (N + 15) / 16;
+    const int nenv = E - e0 < kLrEnvs ? E - e0 : kLrEnvs;
+
+    // No workgroup barrier before the first step: a row wave's LDS tiles are
+    // its own (in-order within the wave), W0 is in its registers, and the
+    // staging buffers are the epilogue waves' alone.
+    if (wave < W) {
+        // ======================= row waves =======================
+        const int e = e0 + c;
+        const bool env_ok = e < E;
+        const unsigned pbase = static_cast<unsigned>(env_ok ? e : 0) * P;
+        unsigned ioff[NKF];
+        double2 wv[NKF], w0v[NKF];
+        float2 av[NKF];
+#if CE_LR_NOCLAMP
+        double xm[NKF];
+        const double *colmax = img + static_cast<unsigned>(ntiles) * TD;
+#endif
+#pragma unroll
+        for (int k = 0; k < NKF; ++k) {
+            const int f = 4 * k + h;
+            ioff[k] = pbase + (f < F ? 2 * f : 0);
+            wv[k] = *reinterpret_cast<const double2 *>(a.W + ioff[k]);
+            av[k] = *reinterpret_cast<const float2 *>(a.act + ioff[k]);
+#if CE_LR_NOCLAMP
+            xm[k] = colmax[f];
+#endif
+        }
+        double xf[TPW][NKF];
+        // W0 (the auto-reset's weights) after the first step's operands: its
+        // loads are not on the way to the first step's row work
+#pragma unroll
+        for (int k = 0; k < NKF; ++k) w0v[k] = *reinterpret_cast<const double2 *>(a.W0 + ioff[k]);
+        unsigned vmask = 0;
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const int t = wave + W * i;
+            const bool live = !PAD || t < ntiles;
+            const double *ti = img + static_cast<unsigned>(live ? t : 0) * TD;
+#pragma unroll
+            for (int k = 0; k < NKF; ++k) xf[i][k] = live ? ti[k * kWave + lane] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xgs[wave][i][q][lane] = live ? ti[(NKF + q) * kWave + lane] : 0.0;
+            if constexpr (PAD) {
+                const int2 ya = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
+                const int2 yb = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
+                const int ys[4] = {ya.x, ya.y, yb.x, yb.y};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) vmask |= (live && ys[q] >= 0 ? 1u : 0u) << (4 * i + q);
+            }
+        }
+        int step_c = a.step[env_ok ? e : 0];
+        double wd[NKF];
+        auto margins = [&]() {
+#pragma unroll
+            for (int k = 0; k < NKF; ++k) {
+                const int f = 4 * k + h;
+                const double w0 = wv[k].x - static_cast<double>(av[k].x);
+                const double w1 = wv[k].y - static_cast<double>(av[k].y);
+                wv[k] = double2{w0, w1};
+                wd[k] = f < F ? w0 - w1 : 0.0;
+            }
+        };
+        margins();
+#ifdef CE_DIAG
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        LP_STAMP(1);
+        constexpr int QC = 4;
+        auto forward = [&](const double (&xv)[NKF]) {
+            lr_d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < NKF; ++k) u = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[k], wd[k], u, 0, 0, 0);
+            return u;
+        };
+        for (int t = 0; t < m.k; ++t) {
+            const int buf = t & 1;
+            float2 an[NKF];
+            {
+                const float *actn = a.act + (t + 1 < m.k ? (t + 1) * m.act_stride : 0);
+#pragma unroll
+                for (int k = 0; k < NKF; ++k) an[k] = *reinterpret_cast<const float2 *>(actn + ioff[k]);
+            }
+#if CE_LR_NOCLAMP
+            double ub = 0.0;
+#pragma unroll
+            for (int k = 0; k < NKF; ++k) ub = fma(fabs(wd[k]), xm[k], ub);
+            ub = fold_pair<16>(ub, ub);
+            ub = fold_pair<32>(ub, ub);
+            const bool bounded = __all(ub < 650.0);
+#else
+            const bool bounded = false;
+#endif
+            lr_d4 sacc[TPW];
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) sacc[i] = lr_d4{0.0, 0.0, 0.0, 0.0};
+            double prod = 1.0, nlog = 0.0, umin = 1.0;
+            int hits = 0;
+            auto post = [&](double uq, double tq, bool valid, double &qo) {
+#if CE_LR_RCP1
+                const double inv = rcp_newton1(1.0 + tq);
+#else
+                const double inv = rcp_unit(1.0 + tq);
+#endif
+                qo = valid ? tq * inv : 0.0;
+                prod *= valid ? inv + 1e-16 : 1.0;
+                {
+                    const double au = valid ? uq : 1.0;
+                    asm("v_min_f64 %0, %1, |%2|" : "=v"(umin) : "v"(umin), "v"(au));
+                }
+                hits += (valid && uq > 0.0) ? 1 : 0;
+            };
+            auto rows = [&](auto clamp_c) {
+#pragma unroll
+                for (int g0 = 0; g0 < TPW; g0 += NG) {
+                    if (g0 > 0) {
+                        nlog -= log_pos(prod);
+                        prod = 1.0;
+                    }
+                    lr_d4 u[NG];
+#pragma unroll
+                    for (int i = 0; i < NG; ++i) u[i] = forward(xf[g0 + i]);
+#pragma unroll
+                    for (int i = 0; i < NG; ++i) {
+                        double gv[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) gv[q] = xgs[wave][g0 + i][q][lane];
+                        double qv[4];
+#pragma unroll
+                        for (int q0 = 0; q0 < 4; q0 += QC) {
+                            double tx[QC];
+#pragma unroll
+                            for (int j = 0; j < QC; ++j) {
+                                if constexpr (decltype(clamp_c)::value) tx[j] = clamp_u(u[i][q0 + j]);
+                                else tx[j] = u[i][q0 + j];
+                            }
+                            exp_neg_q<QC>(tx);
+#pragma unroll
+                            for (int j = 0; j < QC; ++j) {
+                                const bool valid = !PAD || ((vmask >> (4 * (g0 + i) + q0 + j)) & 1u);
+                                post(u[i][q0 + j], tx[j], valid, qv[q0 + j]);
+                            }
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            sacc[g0 + i] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[q], qv[q], sacc[g0 + i], 0, 0, 0);
+                    }
+                }
+            };
+            if (bounded) rows(std::false_type{});
+            else rows(std::true_type{});
+            if (__any(umin < 0x1p-52)) {
+#pragma unroll
+                for (int i = 0; i < TPW; ++i) {
+                    const int tt = wave + W * i;
+                    if (tt >= ntiles) continue;
+                    const double *ti = img + static_cast<unsigned>(tt) * TD;
+                    const int2 ya = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
+                    const int2 yb = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
+                    const int yv[4] = {ya.x, ya.y, yb.x, yb.y};
+                    const lr_d4 uu = forward(xf[i]);
+                    double tx[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) tx[q] = abs_clamp750(uu[q]);
+                    exp_neg_multi_clamped<4>(tx);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (yv[q] >= 0 && tx[q] == 1.0) hits += (yv[q] == 0 ? 1 : 0) - (uu[q] > 0.0 ? 1 : 0);
+                }
+            }
+            double lsum = nlog - log_pos(prod);
+            lsum = fold_pair<16>(lsum, lsum);
+            lsum = fold_pair<32>(lsum, lsum);
+            const double hsum = static_cast<double>(fold_env_lanes(hits));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double v = sacc[0][r];
+#pragma unroll
+                for (int i = 1; i < TPW; ++i) v += sacc[i][r];
+                red_s[buf][wave][r][lane] = v;
+            }
+            if (lane < kLrEnvs) {
+                red_l[buf][wave][lane] = lsum;
+                red_h[buf][wave][lane] = hsum;
+            }
+            {
+                const bool wipe = step_c + 1 >= a.max_steps && a.auto_reset;
+                step_c = wipe ? 0 : step_c + 1;
+#pragma unroll
+                for (int k = 0; k < NKF; ++k)
+                    if (wipe) wv[k] = w0v[k];
+                if (t + 1 < m.k) {
+#pragma unroll
+                    for (int k = 0; k < NKF; ++k) av[k] = an[k];
+                    margins();
+                }
+            }
+            __syncthreads();                                // partials t -> the epilogue waves
+#ifdef CE_DIAG
+            if (t == 0) LP_STAMP(2);
+            if (t == 1) LP_STAMP(3);
+            if (t == m.k - 1) LP_STAMP(4);
+#endif
+        }
+        LP_STAMP(5);
+        __syncthreads();                                    // the epilogue's last obs block
+        if (wave == 0 && env_ok) {
+#pragma unroll
+            for (int k = 0; k < NKF; ++k)
+                if (4 * k + h < F) {
+                    lr_store(a.W + ioff[k], wv[k].x);
+                    lr_store(a.W + ioff[k] + 1, wv[k].y);
+                }
+        }
+    } else {
+        // ==================== epilogue waves ====================
+        const int te = tid - kWave * W;                     // 0 .. EB - 1
+        const int np_ = kLrEnvs * P;
+        const int pmul = (65536 + P - 1) / P;
+        int pj[PR], pp[PR], step_p[PR];
+        bool prole[PR];
+        unsigned gi[PR];
+        double g_prev[PR], rG[PR];
+#pragma unroll
+        for (int r = 0; r < PR; ++r) {
+            const int i = te + r * EB;
+            pj[r] = (i * pmul) >> 16;
+            pp[r] = i - pj[r] * P;
+            prole[r] = i < np_ && e0 + pj[r] < E;
+            gi[r] = static_cast<unsigned>(prole[r] ? e0 + pj[r] : 0) * P + (prole[r] ? pp[r] : 0);
+            g_prev[r] = a.G[gi[r]];
+            step_p[r] = a.step[prole[r] ? e0 + pj[r] : 0];
+        }
+        const int sj = te - (EB - kLrEnvs);
+        const bool srole = sj >= 0 && e0 + sj < E;
+        const unsigned es = srole ? e0 + sj : 0;
+        double lprev = a.L[es];
+        int step_s = a.step[es];
+        const double dB = static_cast<double>(B), rB = a.inv_B;
+        double rL = rcp_newton2(lprev + 0.1);
+#pragma unroll
+        for (int r = 0; r < PR; ++r) rG[r] = rcp_newton2(fabs(g_prev[r]) + 1.0);
+        auto flush_obs = [&](int t) {
+            float *ob = reinterpret_cast<float *>(reinterpret_cast<char *>(a.obs) + t * m.out_step) +
+                        static_cast<unsigned>(e0) * OS;
+            const float *src = obs_s[t & 1];
+            const int nfl = nenv * OS, n4 = nfl >> 2;
+            for (int i = te; i < n4; i += EB) {
+                typedef float lp_f4 __attribute__((ext_vector_type(4)));
+                const lp_f4 v = *reinterpret_cast<const lp_f4 *>(&src[4 * i]);
+                asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(ob + 4 * i), "v"(v) : "memory");
+            }
+            for (int i = 4 * n4 + te; i < nfl; i += EB) lr_store(&ob[i], src[i]);
+        };
+        if (OL == 0)                                        // the weight block of both buffers
+            for (int i = te; i < kLrEnvs * OS; i += EB) {
+                const int j = i / OS, p = i - j * OS;
+                if (p < P) obs_s[0][i] = obs_s[1][i] = 0.0f;
+            }
+        for (int t = 0; t < m.k; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // the row waves' partials of step t
+            if (t > 0) flush_obs(t - 1);
+            const long long ro = t * m.out_step;
+            if (srole) {
+                double lt = 0.0, ht = 0.0;
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    lt += red_l[buf][w][sj];
+                    ht += red_h[buf][w][sj];
+                }
+                const double loss = div_rcp(lt, dB, rB);
+                const double acc = div_rcp(ht, dB, rB);
+                const double lnew = div_rcp(loss - lprev, lprev + 0.1, rL);
+                const int cur = step_s + 1;
+                const bool wipe = cur >= a.max_steps && a.auto_reset;
+                if (a.reward) lr_store(reinterpret_cast<float *>(reinterpret_cast<char *>(a.reward) + ro) + es,
+                                       static_cast<float>(-loss));
+                lr_store(reinterpret_cast<float *>(reinterpret_cast<char *>(a.objective) + ro) + es,
+                         static_cast<float>(loss));
+                lr_store(reinterpret_cast<float *>(reinterpret_cast<char *>(a.accuracy) + ro) + es,
+                         static_cast<float>(acc));
+                if (a.done) (reinterpret_cast<uint8_t *>(a.done) + ro)[es] = cur >= a.max_steps ? 1 : 0;
+                lr_store(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro) + es, cur);
+                obs_s[buf][sj * OS + P - OL] = wipe ? 0.0f : static_cast<float>(lnew);
+                lprev = wipe ? 0.0 : lnew;
+                step_s = wipe ? 0 : cur;
+                rL = rcp_newton2(lprev + 0.1);
+            }
+#pragma unroll
+            for (int r = 0; r < PR; ++r) {
+                if (!prole[r]) continue;
+                const bool wipe = step_p[r] + 1 >= a.max_steps && a.auto_reset;
+                const int f = pp[r] >> 1;
+                double sf = 0.0;
+#pragma unroll
+                for (int w = 0; w < W; ++w) sf += red_s[buf][w][f >> 2][pj[r] + 16 * (f & 3)];
+                const double g = div_rcp((pp[r] & 1) ? sf : -sf, dB, rB);
+                const double gnew = div_rcp(g, fabs(g_prev[r]) + 1.0, rG[r]);
+                obs_s[buf][pj[r] * OS + P + 1 + pp[r] - OL] = wipe ? 0.0f : static_cast<float>(gnew);
+                g_prev[r] = wipe ? 0.0 : gnew;
+                step_p[r] = wipe ? 0 : step_p[r] + 1;
+                rG[r] = rcp_newton2(fabs(g_prev[r]) + 1.0);
+            }
+        }
+        __syncthreads();                                    // the last step's obs block staged
+        if (m.k > 0) flush_obs(m.k - 1);
+#pragma unroll
+        for (int r = 0; r < PR; ++r)
+            if (prole[r]) lr_store(&a.G[gi[r]], g_prev[r]);
+        if (srole) {
+            lr_store(&a.L[es], lprev);
+            lr_store(&a.step[es], step_s);
+        }
+    }
+#ifdef CE_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LP_STAMP(6);
+    const int row = blockIdx.x * 8 + wave;                  // 8 stamp rows per workgroup
+    if (row < E && lane < 8) a.diag[static_cast<size_t>(row) * 8 + lane] = lp_st[lane];
+#endif
+}
+
 }  // namespace ce

@@ -7,6 +7,7 @@
 #include "optimize_lr_persist.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace ce {
 
@@ -19,6 +20,38 @@ void launch_persist(const StepArgs<double> &a, const ManyArgs &m, hipStream_t st
     const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
     hipLaunchKernelGGL((optimize_lr_persist_kernel<NKF, TPW, PAD, W>), dim3(grid), dim3(kWave * W), 0,
                        stream, a, m);
+}
+
+template <int NKF, int TPW, bool PAD>
+void launch_persist_ws(const StepArgs<double> &a, const ManyArgs &m, hipStream_t stream) {
+    const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
+    hipLaunchKernelGGL((optimize_lr_persist_ws_kernel<NKF, TPW, PAD>), dim3(grid), dim3(512), 0, stream,
+                       a, m);
+}
+
+template <int NKF, bool PAD>
+constexpr PersistFn kWsByTpw[3] = {launch_persist_ws<NKF, 1, PAD>, launch_persist_ws<NKF, 2, PAD>,
+                                   launch_persist_ws<NKF, 4, PAD>};
+
+template <bool PAD>
+PersistFn pick_ws(int nkf, int tpw) {
+    const int i = tpw == 1 ? 0 : tpw == 2 ? 1 : 2;
+    switch (nkf) {
+        case 1: return kWsByTpw<1, PAD>[i];
+        case 2: return kWsByTpw<2, PAD>[i];
+        case 3: return kWsByTpw<3, PAD>[i];
+        default: return kWsByTpw<4, PAD>[i];
+    }
+}
+
+// the wave-specialised form (row waves + epilogue waves): CE_LP_FORM=plain
+// selects the all-roles form instead (A/B runs)
+bool lp_ws() {
+    static const bool ws = [] {
+        const char *v = std::getenv("CE_LP_FORM");
+        return !(v && std::strcmp(v, "plain") == 0);
+    }();
+    return ws;
 }
 
 template <int NKF, bool PAD, int W>
@@ -67,12 +100,19 @@ void lr_launch_persist(const StepArgs<double> &a, int k, long long act_stride, l
         return;
     }
     const int tpw = lp_tpw(a.N);
+    if (lp_ws() && tpw <= 4) {   // 8 tiles per wave do not fit two waves per SIMD
+        (lp_pad(a.N) ? pick_ws<true>(nkf, tpw) : pick_ws<false>(nkf, tpw))(a, m, stream);
+        return;
+    }
     (lp_pad(a.N) ? pick<true, 4>(nkf, tpw) : pick<false, 4>(nkf, tpw))(a, m, stream);
 }
 
 std::string lr_persist_name(int n_rows, int n_features) {
     const int nkf = lr_nkf(n_features);
     const int w = lp_waves(nkf) == 8 && lp_tpw(n_rows, 8) > 0 && lp_tpw(n_rows, 8) <= 4 ? 8 : 4;
+    if (w == 4 && lp_ws() && lp_tpw(n_rows) <= 4)
+        return "optimize_lr_persist_ws_kernel<" + std::to_string(nkf) + "," +
+               std::to_string(lp_tpw(n_rows)) + "," + (lp_pad(n_rows) ? "true" : "false") + ">";
     return "optimize_lr_persist_kernel<" + std::to_string(nkf) + "," +
            std::to_string(lp_tpw(n_rows, w)) + "," + (lp_pad(n_rows, w) ? "true" : "false") + "," +
            std::to_string(w) + ">";

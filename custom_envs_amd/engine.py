@@ -306,7 +306,7 @@ class OptimizeEngine:
 
     @property
     def persistent(self):
-        return self.many_kernel.startswith('optimize_lr_persist_kernel')
+        return self.many_kernel.startswith('optimize_lr_persist')
 
     def alloc_rollout(self, k, torch_device=None):
         """A [k] array of output records for ``rollout_device``: one byte

@@ -52,7 +52,7 @@ def main():
             st = np.zeros((E, 8), np.uint64)
             _native.check(lib.ce_diag_stamps(eng._h, st.ctypes.data), 'diag')
             st = st.astype(np.int64)
-            st = st[st[:, 0] != 0]
+            st = st[(st[:, 0] != 0) & (st[:, 1] != 0)]    # row waves (ws form: not the epilogue waves)
             rows.append(st)
         st = np.concatenate(rows)
         us = lambda d: float(np.median(d)) / 100.0     # 10 ns ticks

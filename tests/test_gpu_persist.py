@@ -81,7 +81,7 @@ def test_benchmark_shape_bit_equal_to_one_step_launches(lr_dataset):
     got_per, st_per = _rollout(per, range(E), acts, [20, 20, 5])
     per.close()
     eng = _engine(lr_dataset, E)
-    assert eng.many_kernel == 'optimize_lr_persist_kernel<3,4,false,4>'
+    assert eng.many_kernel == 'optimize_lr_persist_ws_kernel<3,4,false>'
     got, st = _rollout(eng, range(E), acts, [20, 20, 5])
     eng.close()
     for name in FIELDS:
@@ -177,10 +177,10 @@ def test_1000_steps_every_slot_against_oracle(lr_dataset):
 
 
 @pytest.mark.parametrize('n_rows,n_features,kernel', [
-    (64, 10, 'optimize_lr_persist_kernel<3,1,false,4>'),
-    (40, 10, 'optimize_lr_persist_kernel<3,1,true,4>'),
-    (100, 4, 'optimize_lr_persist_kernel<1,2,true,4>'),
-    (128, 16, 'optimize_lr_persist_kernel<4,2,false,4>'),
+    (64, 10, 'optimize_lr_persist_ws_kernel<3,1,false>'),
+    (40, 10, 'optimize_lr_persist_ws_kernel<3,1,true>'),
+    (100, 4, 'optimize_lr_persist_ws_kernel<1,2,true>'),
+    (128, 16, 'optimize_lr_persist_ws_kernel<4,2,false>'),
     (512, 7, 'optimize_lr_persist_kernel<2,8,false,4>'),
     (300, 13, 'optimize_lr_persist_kernel<4,8,true,4>'),
 ])
