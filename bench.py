@@ -1070,7 +1070,7 @@ def multi_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, shard
     bpe = multi_bytes_per_env_step(P, H)
     achieved_gbs = bpe * E / (kernel_ms * 1e-3) / 1e9
     kernel = getattr(eng, 'many_kernel', 'multi_step_kernel<4>')
-    persistent = kernel.startswith('multi_persist_kernel')
+    persistent = kernel.startswith('multi_persist')
     # a persistent launch of S steps moves per env-step the actions 4P and
     # the outputs (obs 12HP, reward 4P, done P, info 56, length 4); the state
     # (theta, g, the raw ring 5(1 + 2P), the adjusted ring H(1 + 2P) floats +

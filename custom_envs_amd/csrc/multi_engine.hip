@@ -45,9 +45,24 @@ void launch_multi_step(const ce::MultiArgs &a, int, hipStream_t s) {
 }
 // K steps in one launch (multi_persist_kernel): the reference default history
 // H = 5 only (the compile-time instance the kernel needs)
+// the two-wave form (state wave + output wave); CE_MULTI_FORM=one runs the
+// one-wave form (A/B)
+bool multi_two_wave() {
+    static const bool two = [] {
+        const char *v = std::getenv("CE_MULTI_FORM");
+        return !(v && std::strcmp(v, "one") == 0);
+    }();
+    return two;
+}
 template <int P>
 void launch_multi_persist(const ce::MultiArgs &a, int k, long long act_stride, long long out_step,
                           hipStream_t s) {
+    if (multi_two_wave()) {
+        const long lanes = static_cast<long>(a.E) * ce::Group<P>::G;
+        hipLaunchKernelGGL((ce::multi_persist2_kernel<P, 5>), dim3(static_cast<int>((lanes + 63) / 64)),
+                           dim3(128), 0, s, a, k, act_stride, out_step);
+        return;
+    }
     const size_t lds = ce::kMultiBlock / 64 * (64 / ce::Group<P>::G) * P * 3 * 5 * sizeof(float);
     hipLaunchKernelGGL((ce::multi_persist_kernel<P, 5>), dim3(multi_grid<P>(a.E)), dim3(ce::kMultiBlock),
                        lds, s, a, k, act_stride, out_step);
@@ -223,7 +238,8 @@ int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out) {
     if (const char *pe = std::getenv("CE_PERSIST")) e->persist_on = pe[0] != '0';
     e->step_name = "multi_step_kernel<" + std::to_string(cfg->n_params) + "," +
                    std::to_string(cfg->max_history == 5 ? 5 : 0) + ">";
-    e->many_name = "multi_persist_kernel<" + std::to_string(cfg->n_params) + ",5>";
+    e->many_name = std::string(multi_two_wave() ? "multi_persist2_kernel<" : "multi_persist_kernel<") +
+                   std::to_string(cfg->n_params) + ",5>";
     auto bail = [&](int code) {
         ce_multi_destroy(e);
         return code;

@@ -748,3 +748,279 @@ __global__ __launch_bounds__(kMultiBlock) void multi_persist_kernel(MultiArgs a,
 }
 
 }  // namespace ce
+
+namespace ce {
+
+// The two-wave form of multi_persist_kernel: the same 64 / G envs per
+// workgroup, their lanes mirrored in TWO waves on two SIMDs.  The STATE wave
+// runs the loop-carried chain (the update, the Rosenbrock pair, the three
+// observation ratios, the ring updates) and stages the step's observation
+// rows in LDS; the OUTPUT wave takes each step's per-lane results from LDS
+// and does everything nothing later depends on -- the observation rows'
+// copy-out, the fourteen info reductions, reward / done / length.  One wave
+// was latency-bound on the sum of both (≈1.7 us per 1024-env step); split,
+// a step costs about the longer half.  LDS hand-over double-buffered by step
+// parity behind one 128-thread barrier per step.  Same arithmetic, same
+// operation order as multi_persist_kernel: bit-identical outputs.
+struct MultiXch {
+    double adj_g, adj_l, gsum, lsum, st_abs, reward;
+    float thn, lr, g, gp, loss;
+    int s, terminal;
+};
+
+template <int P, int HC>
+__global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K, long long act_stride,
+                                                            long long out_step) {
+#pragma clang fp contract(off)
+    constexpr int G = Group<P>::G;
+    constexpr int H = HC;
+    constexpr int row = 3 * H;
+    static_assert(HC > 0 && HC <= kMultiStageH, "compile-time history");
+    constexpr int span = 64 / G * P * row;                  // floats of the workgroup's env block
+    __shared__ __attribute__((aligned(16))) float stage[2][span];
+    __shared__ MultiXch xch[2][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t gt = static_cast<size_t>(blockIdx.x) * 64 + lane;   // the lane's (env, agent)
+    const size_t e = gt / G;
+    const int i = static_cast<int>(gt % G);
+    const size_t E = a.E;
+    const bool env_ok = e < E;
+    const bool on = env_ok && i < P;
+    const size_t ec = env_ok ? e : 0;
+    const int ic = i < P ? i : 0;
+    const int r = P <= 10 ? ic : a.agent_row[ic];
+    const unsigned Eu = static_cast<unsigned>(E), eu = static_cast<unsigned>(ec);
+    const unsigned ep = eu * P + ic;
+    const size_t e_first = static_cast<size_t>(blockIdx.x) * 64 / G;
+    const size_t envs = e_first < E ? (E - e_first < static_cast<size_t>(64 / G) ? E - e_first
+                                                                                  : static_cast<size_t>(64 / G))
+                                    : 0;
+    const int nblk = static_cast<int>(envs) * P * row;
+
+    if (wave == 0) {
+        // ======================= state wave =======================
+        int s_prev = at32(a.step, eu);
+        float act = at32(a.act, eu * P + r);
+        const float th_init = i < P ? a.init[i] : 0.0f;
+        const float g_init = i < P ? a.init_g[i] : 0.0f, l_init = a.init_l;
+        float th = at32(a.theta, ep);
+        float gc = at32(a.grad, ep);
+        float hl_v[kRawHist], hg_v[kRawHist], hw_v[kRawHist];
+#pragma unroll
+        for (int k = 0; k < kRawHist; ++k) {
+            hl_v[k] = at32(a.hl, k * Eu + eu);
+            hg_v[k] = at32(a.hg, k * Eu * P + ep);
+            hw_v[k] = at32(a.hw, k * Eu * P + ep);
+        }
+        float ol_v[H], og_v[H], ow_v[H];
+        double sa_v[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            ol_v[j] = at32(a.ol, j * Eu + eu);
+            og_v[j] = at32(a.og, j * Eu * P + ep);
+            ow_v[j] = at32(a.ow, j * Eu * P + ep);
+            sa_v[j] = at32(a.sa, j * Eu * P + ep);
+        }
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            const float act_next = at32(a.act + (t + 1 < K ? (t + 1) * act_stride : 0), eu * P + r);
+            const int s = s_prev + 1;
+            const float x = act - 4.0f;
+            const float lr = static_cast<float>(exp10(static_cast<double>(x)));
+            const float thn = th - gc * lr;
+            float g, loss;
+            rosenbrock_lane<P>(thn, i, g, loss);
+            const int slot = s % kRawHist, prev = (s - 1) % kRawHist;
+            double l_prev = 0.0;
+            float gp = 0.0f, wp = 0.0f;
+            double lsum = loss, gsum = g;
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k) {
+                if (k == prev) {
+                    l_prev = hl_v[k];
+                    gp = hg_v[k];
+                    wp = hw_v[k];
+                }
+                if (k != slot) {
+                    lsum += hl_v[k];
+                    gsum += hg_v[k];
+                }
+            }
+            const double adj_l = ratio_fast(loss, static_cast<float>(l_prev));
+            const double adj_g = ratio_fast(g, gp);
+            const double adj_w = ratio_fast(thn, wp);
+            const float nw = static_cast<float>(clip100(adj_w) - 1.0);
+            const float nl = static_cast<float>(clip100(adj_l) - 1.0);
+            const float ng = static_cast<float>(clip100(adj_g) - 1.0);
+            const double nsum = fabs(adj_w) + fabs(adj_g) + fabs(adj_l);
+            const int aslot = (s - 1) % H;
+            double reward = 1.0 - adj_l;
+            reward = reward < -100.0 ? -100.0 : (reward > 100.0 ? 100.0 : reward);
+            bool terminal = s >= a.max_batches;
+            if (!terminal && loss > 1e4f) {
+                terminal = true;
+                reward -= static_cast<double>(a.max_batches - s);
+            }
+            const bool wipe = terminal && a.auto_reset;
+            double st_abs = 0.0;
+            const int k0 = aslot;
+            float *const lrow = stage[buf] + ((lane / G) * P + r) * row;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const int kk = k0 - j >= 0 ? k0 - j : k0 - j + H;
+                float wk = ow_v[j], gk = og_v[j], lk = ol_v[j];
+                double sk = sa_v[j];
+                if (kk == 0) {
+                    wk = nw;
+                    gk = ng;
+                    lk = nl;
+                    sk = nsum;
+                }
+                st_abs += sk;
+                if (on) {
+                    lrow[kk] = wipe ? -1.0f : wk;
+                    lrow[H + kk] = wipe ? -1.0f : lk;
+                    lrow[2 * H + kk] = wipe ? -1.0f : gk;
+                }
+            }
+            MultiXch &xo = xch[buf][lane];
+            xo.adj_g = adj_g;
+            xo.adj_l = adj_l;
+            xo.gsum = gsum;
+            xo.lsum = lsum;
+            xo.st_abs = st_abs;
+            xo.reward = reward;
+            xo.thn = thn;
+            xo.lr = lr;
+            xo.g = g;
+            xo.gp = gp;
+            xo.loss = loss;
+            xo.s = s;
+            xo.terminal = terminal ? 1 : 0;
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k)
+                if (k == slot) {
+                    hg_v[k] = g;
+                    hw_v[k] = thn;
+                    hl_v[k] = loss;
+                }
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+                if (j == aslot) {
+                    og_v[j] = ng;
+                    ow_v[j] = nw;
+                    sa_v[j] = nsum;
+                    ol_v[j] = nl;
+                }
+            if (wipe) {
+#pragma unroll
+                for (int k = 0; k < kRawHist; ++k) {
+                    hg_v[k] = k == 0 ? g_init : 0.0f;
+                    hw_v[k] = k == 0 ? th_init : 0.0f;
+                    hl_v[k] = k == 0 ? l_init : 0.0f;
+                }
+#pragma unroll
+                for (int j = 0; j < H; ++j) {
+                    og_v[j] = -1.0f;
+                    ow_v[j] = -1.0f;
+                    ol_v[j] = -1.0f;
+                    sa_v[j] = 0.0;
+                }
+                th = th_init;
+                gc = g_init;
+                s_prev = 0;
+            } else {
+                th = thn;
+                gc = g;
+                s_prev = s;
+            }
+            act = act_next;
+            __syncthreads();                                // step t's rows and results -> the output wave
+        }
+        if (on) {
+            at32(a.theta, ep) = th;
+            at32(a.grad, ep) = gc;
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k) {
+                at32(a.hg, k * Eu * P + ep) = hg_v[k];
+                at32(a.hw, k * Eu * P + ep) = hw_v[k];
+                if (i == 0) at32(a.hl, k * Eu + eu) = hl_v[k];
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                at32(a.og, j * Eu * P + ep) = og_v[j];
+                at32(a.ow, j * Eu * P + ep) = ow_v[j];
+                at32(a.sa, j * Eu * P + ep) = sa_v[j];
+                if (i == 0) at32(a.ol, j * Eu + eu) = ol_v[j];
+            }
+            if (i == 0) at32(a.step, eu) = s_prev;
+        }
+    } else {
+        // ======================= output wave =======================
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // step t's rows and results staged
+            const long long ro = t * out_step;
+            {
+                const float *lds = stage[buf];
+                float *out = reinterpret_cast<float *>(reinterpret_cast<char *>(a.obs) + ro) + e_first * P * row;
+                constexpr int kV = (span / 4 + 63) / 64;
+                if ((nblk & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+                    const float4 *src = reinterpret_cast<const float4 *>(lds);
+                    float4 *dst4 = reinterpret_cast<float4 *>(out);
+                    const int n4 = nblk >> 2;
+                    float4 v[kV];
+#pragma unroll
+                    for (int u = 0; u < kV; ++u) {
+                        const int q = lane + 64 * u;
+                        v[u] = src[q < n4 ? q : n4 - 1];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kV; ++u) {
+                        const int q = lane + 64 * u;
+                        if (q < n4) dst4[q] = v[u];
+                    }
+                } else {
+                    for (int q = lane; q < nblk; q += 64) out[q] = lds[q];
+                }
+            }
+            const MultiXch xi = xch[buf][lane];
+            const double thn = xi.thn, lr = xi.lr;
+            auto mine = [&](double v) { return on ? v : 0.0; };
+            const double wsum = group_sum<G>(mine(fabs(thn)));
+            const double amean = group_sum<G>(mine(lr)) / P;
+            const double dev = lr - amean;
+            const double avar = group_sum<G>(mine(dev * dev)) / P;
+            const double adjg = group_sum<G>(mine(fabs(xi.adj_g))) / P;
+            const double gdiff = group_sum<G>(mine(fabs(static_cast<double>(xi.g) - static_cast<double>(xi.gp)))) / P;
+            const double gsum_all = group_sum<G>(mine(xi.gsum));
+            const double st_all = group_sum<G>(mine(xi.st_abs));
+            if (on) {
+                const bool terminal = xi.terminal != 0;
+                if (i == 0) {
+                    float *info = reinterpret_cast<float *>(reinterpret_cast<char *>(a.info) + ro) + eu * kMultiInfo;
+                    info[0] = terminal ? xi.loss : __builtin_nanf("");
+                    info[1] = xi.loss;
+                    info[2] = static_cast<float>(wsum / P);
+                    info[3] = static_cast<float>(wsum);
+                    info[4] = static_cast<float>(amean);
+                    info[5] = static_cast<float>(sqrt(avar));
+                    info[6] = static_cast<float>(st_all / (P * row));
+                    info[7] = static_cast<float>(st_all);
+                    info[8] = static_cast<float>(gsum_all / (kRawHist * P));
+                    info[9] = static_cast<float>(gsum_all);
+                    info[10] = static_cast<float>(xi.lsum / kRawHist);
+                    info[11] = static_cast<float>(xi.adj_l);
+                    info[12] = static_cast<float>(adjg);
+                    info[13] = static_cast<float>(gdiff);
+                    at32(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro), eu) = xi.s;
+                }
+                at32(reinterpret_cast<float *>(reinterpret_cast<char *>(a.reward) + ro), eu * P + r) =
+                    static_cast<float>(xi.reward);
+                at32(reinterpret_cast<uint8_t *>(a.done) + ro, eu * P + r) = terminal ? 1 : 0;
+            }
+        }
+    }
+}
+
+}  // namespace ce

@@ -87,7 +87,7 @@ class MultiOptEngine:
 
     @property
     def persistent(self):
-        return self.many_kernel.startswith('multi_persist_kernel')
+        return self.many_kernel.startswith('multi_persist')
 
     def alloc_rollout(self, k, torch_device=None):
         """[k] output records (256-B aligned field segments per record):
