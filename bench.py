@@ -872,8 +872,11 @@ def main():
             line['gather_record'] = 'compact' if shard.compact else 'full'
             line['gather_mode'] = gather_mode
             line['gather_graph'] = gather_graph
-        bpe = line['roofline'].get('bytes_per_env_step', line['roofline'].get('hbm', {}).get(
-            'bytes_per_env_step'))
+        # the traffic is compared with what the launch form must move
+        # (persistent: the state once per launch), else the per-step count
+        r = line['roofline']
+        bpe = r.get('bytes_per_env_step_moved', r.get('hbm', {}).get('bytes_per_env_step_moved',
+                    r.get('bytes_per_env_step', r.get('hbm', {}).get('bytes_per_env_step'))))
         line['roofline'].update(traffic_fields(args, eng, E, bpe if isinstance(bpe, (int, float)) else None))
         line['cpu_baseline'] = cpu
         if host_rate is not None:

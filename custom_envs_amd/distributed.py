@@ -221,6 +221,7 @@ class ShardedEnvs:
         self.outs = [self.layout.views(b, engine.num_envs) for b in self.buffers]
         # every record of every slot: what a K-step rollout writes
         self.slabs = [self.layout.chunk_views(b, engine.num_envs, self.chunk) for b in self.buffers]
+        self._partial = {}                 # receive buffers of shorter gathers, by (slot, k)
 
     @property
     def buffer(self):
@@ -283,8 +284,13 @@ class ShardedEnvs:
                 work = dist.all_gather_into_tensor(gathered, self.buffers[slot], group=self.group,
                                                    async_op=async_op)
             else:
-                gathered, stride = torch.empty(world * k * nb, dtype=torch.uint8,
-                                               device=self.buffers[slot].device), k * nb
+                # a persistent receive buffer per (slot, k): no allocation per
+                # call (and none inside a captured graph)
+                key = (slot, k)
+                if key not in self._partial:
+                    self._partial[key] = torch.empty(world * k * nb, dtype=torch.uint8,
+                                                     device=self.buffers[slot].device)
+                gathered, stride = self._partial[key], k * nb
                 work = dist.all_gather_into_tensor(gathered, self.buffers[slot][:k * nb],
                                                    group=self.group, async_op=async_op)
         counts = self.counts if self.collective else [self.hi - self.lo]
