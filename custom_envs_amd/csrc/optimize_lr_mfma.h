@@ -78,6 +78,13 @@ typedef double lr_d4 __attribute__((ext_vector_type(4)));
 #ifndef CE_LR_OBS_STAGE
 #define CE_LR_OBS_STAGE 1
 #endif
+//  CE_LR_TEXP     e^-u through a 256-entry table of 2^(j/256) and a degree-4
+//                 polynomial (exp_neg_tab, 10 f64 operations per value)
+//                 instead of the degree-10 polynomial over [-ln2/2, ln2/2]
+//                 (exp_neg_q, 15): the row work is f64-pipe bound
+#ifndef CE_LR_TEXP
+#define CE_LR_TEXP 1
+#endif
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
 
@@ -109,7 +116,8 @@ __host__ __device__ constexpr int lr_tile_doubles(int nkf) { return (nkf + 4 + 2
 //   [nkf + 5]  int32 pair: q = 2, 3
 // (layout [tile][slot][lane]; built by the engine at ce_create), then
 // kLrMaxF doubles: max over rows of |x[r][f]| (0 past F), the column maxima
-// of the |u| bound (CE_LR_NOCLAMP)
+// of the |u| bound (CE_LR_NOCLAMP), then the kLrExpTab entries 2^(j/256) of
+// exp_neg_tab
 
 // MODE (lr_mode): 0 = one tile at a time, padding rows (label -1) masked
 // out of every statistic; 1 = N a multiple of 16 and every wave owning the
@@ -188,6 +196,63 @@ __device__ __forceinline__ void exp_neg_q(double (&a)[Q]) {
         a[i] = ldexp(q[i], static_cast<int>(static_cast<unsigned long long>(__double_as_longlong(big[i]))));
 }
 
+// e^-x for Q arguments x in [-700, 750] through a table of 2^(j/256)
+// (CE_LR_TEXP): m = rint(-256 x log2e) by the shifter, r = -x - m ln2/256 in
+// [-ln2/512, ln2/512], e^r - 1 = r + r^2/2 + r^3/6 + r^4/24 (truncation
+// |r|^5/120 < 4e-17 relative), e^-x = 2^(m >> 8) (T[m & 255] + T[m & 255] (e^r - 1)).
+// 10 f64 operations per value against exp_neg_q's 15; the table entry is an
+// LDS read under the polynomial.  T[j] is 2^(j/256) rounded to float64
+// (lr_build_image), so the result is within ~1.5 ulp (exp_neg_q: 3 ulp).
+constexpr int kLrExpTab = 256;
+template <int Q>
+__device__ __forceinline__ void exp_neg_tab(double (&a)[Q], const double *tab) {
+    constexpr double kShift = 0x1.8p52;
+    constexpr double kC = kLog2e * kLrExpTab;           // exact: power-of-two scale
+    constexpr double kH = kLn2Hi / kLrExpTab, kL = kLn2Lo / kLrExpTab;
+    double big[Q], r[Q], p[Q], t[Q];
+    int n[Q];
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+        big[i] = fma(a[i], -kC, kShift);
+        const double m = big[i] - kShift;
+        r[i] = fma(m, -kL, fma(m, -kH, -a[i]));       // m kH exact: |m| < 2^19, kH 32 bits
+        const int lo = static_cast<int>(static_cast<unsigned>(__double_as_longlong(big[i])));
+        t[i] = tab[lo & (kLrExpTab - 1)];
+        n[i] = lo >> 8;                                 // floor(m / 256)
+    }
+#pragma unroll
+    for (int i = 0; i < Q; ++i) p[i] = fma(r[i], 1.0 / 24.0, 1.0 / 6.0);
+#pragma unroll
+    for (int i = 0; i < Q; ++i) p[i] = fma(p[i], r[i], 0.5);
+#pragma unroll
+    for (int i = 0; i < Q; ++i) p[i] = fma(p[i], r[i], 1.0);
+#pragma unroll
+    for (int i = 0; i < Q; ++i) p[i] *= r[i];
+#pragma unroll
+    for (int i = 0; i < Q; ++i) a[i] = ldexp(fma(t[i], p[i], t[i]), n[i]);
+}
+
+// The wave's LDS copy of the table (entries lane + 64 i): in-order LDS
+// within a wave, so no barrier before its first use
+__device__ __forceinline__ void lr_exp_table(const double *src, double *tab, int lane) {
+    double v[kLrExpTab / kWave];
+#pragma unroll
+    for (int i = 0; i < kLrExpTab / kWave; ++i) v[i] = src[lane + kWave * i];
+#pragma unroll
+    for (int i = 0; i < kLrExpTab / kWave; ++i) tab[lane + kWave * i] = v[i];
+}
+
+// the row loops' exponential: the table form, or exp_neg_q (CE_LR_TEXP=0)
+template <int Q>
+__device__ __forceinline__ void lr_exp_neg(double (&a)[Q], const double *tab) {
+#if CE_LR_TEXP
+    exp_neg_tab<Q>(a, tab);
+#else
+    (void)tab;
+    exp_neg_q<Q>(a);
+#endif
+}
+
 // sum of an int over lanes l, l^16, l^32, l^48 (permlane swaps)
 __device__ __forceinline__ int fold_env_lanes(int v) {
     unsigned x = static_cast<unsigned>(v), y = x;
@@ -224,6 +289,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
 #if CE_LR_OBS_STAGE
     __shared__ __attribute__((aligned(16))) float obs_s[kLrEnvs * (2 * P_MAX + 4)];
 #endif
+    __shared__ double tab_s[kLrWaves][CE_LR_TEXP ? kLrExpTab : 1];   // per-wave exp tables
 #ifdef CE_DIAG
     unsigned long long stamps[kStamps] = {0};
     stamps[6] = __builtin_amdgcn_s_memrealtime();
@@ -295,6 +361,10 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     // the first group's tile loads right behind W and the action: the
     // G / step / L loads below are the epilogue's and may wait
     load_group(wave < ntiles ? wave : 0);              // unconditional: no merge-point vmcnt(0)
+#if CE_LR_TEXP
+    // the exp table behind the image's column maxima, into the wave's LDS copy
+    lr_exp_table(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tab_s[wave], lane);
+#endif
     const int np_ = kLrEnvs * P;
     const int pmul = (65536 + P - 1) / P;              // a.p_mul, formed here (uniform)
     int pj[PR], pp[PR], step_p[PR];
@@ -433,7 +503,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
                 if constexpr (decltype(clamp_c)::value) tx[i] = clamp_u(u[q0 + i]);
                 else tx[i] = u[q0 + i];
             }
-            exp_neg_q<QC>(tx);                          // t = e^-u
+            lr_exp_neg<QC>(tx, tab_s[wave]);            // t = e^-u
 #pragma unroll
             for (int i = 0; i < QC; ++i) post(u[q0 + i], tx[i], ys[q0 + i], qv[q0 + i]);
         }

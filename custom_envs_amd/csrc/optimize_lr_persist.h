@@ -84,6 +84,7 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
     __shared__ double red_l[2][W][kLrEnvs];                 // per-wave -log CE partials
     __shared__ double red_h[2][W][kLrEnvs];                 // per-wave hit counts
     __shared__ __attribute__((aligned(16))) float obs_s[2][kLrEnvs * OSM];
+    __shared__ double tab_s[W][CE_LR_TEXP ? kLrExpTab : 1];   // per-wave exp tables
 
 #ifdef CE_DIAG
     unsigned long long lp_st[8] = {0};
@@ -141,6 +142,9 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
             for (int q = 0; q < 4; ++q) vmask |= (live && ys[q] >= 0 ? 1u : 0u) << (4 * i + q);
         }
     }
+#if CE_LR_TEXP
+    lr_exp_table(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tab_s[wave], lane);
+#endif
     int step_c = a.step[env_ok ? e : 0];                    // env c's counter (the wipe of wv)
     // role "parameter": index i = j P + p < 16 P, i = tid + r BLK
     const int np_ = kLrEnvs * P;
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
                             if constexpr (decltype(clamp_c)::value) tx[j] = clamp_u(u[i][q0 + j]);
                             else tx[j] = u[i][q0 + j];
                         }
-                        exp_neg_q<QC>(tx);                  // t = e^-u
+                        lr_exp_neg<QC>(tx, tab_s[wave]);                  // t = e^-u
 #pragma unroll
                         for (int j = 0; j < QC; ++j) {
                             const bool valid = !PAD || ((vmask >> (4 * (g0 + i) + q0 + j)) & 1u);
@@ -460,6 +464,7 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
     __shared__ double red_h[2][W][kLrEnvs];
     __shared__ __attribute__((aligned(16))) float obs_s[2][kLrEnvs * OSM];
     __shared__ double xgs[W][TPW][4][kWave];                // gradient A operands
+    __shared__ double tab_s[W][CE_LR_TEXP ? kLrExpTab : 1];   // the row waves' exp tables
 
 #ifdef CE_DIAG
     unsigned long long lp_st[8] = {0};
@@ -524,6 +529,9 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                 for (int q = 0; q < 4; ++q) vmask |= (live && ys[q] >= 0 ? 1u : 0u) << (4 * i + q);
             }
         }
+#if CE_LR_TEXP
+        lr_exp_table(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tab_s[wave], lane);
+#endif
         int step_c = a.step[env_ok ? e : 0];
         double wd[NKF];
         auto margins = [&]() {
@@ -609,7 +617,7 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                                 if constexpr (decltype(clamp_c)::value) tx[j] = clamp_u(u[i][q0 + j]);
                                 else tx[j] = u[i][q0 + j];
                             }
-                            exp_neg_q<QC>(tx);
+                            lr_exp_neg<QC>(tx, tab_s[wave]);
 #pragma unroll
                             for (int j = 0; j < QC; ++j) {
                                 const bool valid = !PAD || ((vmask >> (4 * (g0 + i) + q0 + j)) & 1u);

@@ -155,7 +155,8 @@ constexpr GenFn kLrSteps[4] = {launch_lr<1>, launch_lr<2>, launch_lr<3>, launch_
 bool lr_shape_ok(int n_features, int n_classes) { return lr_mfma_shape(n_features, n_classes); }
 
 size_t lr_image_doubles(int n_features, int n_rows) {
-    return static_cast<size_t>((n_rows + 15) / 16) * lr_tile_doubles(lr_nkf(n_features)) + kLrMaxF;
+    return static_cast<size_t>((n_rows + 15) / 16) * lr_tile_doubles(lr_nkf(n_features)) + kLrMaxF +
+           kLrExpTab;
 }
 
 void lr_build_image(int F, int N, const double *x, const int32_t *y, double *img) {
@@ -184,6 +185,9 @@ void lr_build_image(int F, int N, const double *x, const int32_t *y, double *img
         for (int r = 0; f < F && r < N; ++r) m = std::max(m, std::fabs(x[static_cast<size_t>(r) * F + f]));
         colmax[f] = m;
     }
+    // then T[j] = 2^(j/256), rounded to float64 (exp_neg_tab)
+    double *tab = colmax + kLrMaxF;
+    for (int j = 0; j < kLrExpTab; ++j) tab[j] = static_cast<double>(exp2l(static_cast<long double>(j) / kLrExpTab));
 }
 
 void lr_launch_step(const StepArgs<double> &a, hipStream_t stream) {
