@@ -157,6 +157,10 @@ def parse(argv=None):
                    help='rank 0 at N = 1: measure roofline.traffic in this run (two rocprofv3 '
                         '--pmc passes of this workload as child processes, scripts/traffic.py); '
                         'the default when rocprofv3 is on PATH')
+    p.add_argument('--repeat-timed', type=int, default=0,
+                   help='diagnostic: after the timed region, time the same K steps R more '
+                        'times (same bracket) and list them as timed_repeats_ms; value stays '
+                        'the first measurement')
     p.add_argument('--no-measure-traffic', dest='measure_traffic', action='store_false',
                    help='take roofline.traffic from the committed '
                         'profiles/<round>_traffic_<workload>.json instead')
@@ -789,6 +793,9 @@ def main():
         primary(args.warmup)
         torch.cuda.synchronize()
         elapsed = _timed(torch, dist, primary, args.steps)
+        if args.repeat_timed > 0:
+            modes['timed_repeats'] = [_timed(torch, dist, primary, args.steps)
+                                      for _ in range(args.repeat_timed)]
         if slab is not None:
             # the same steps as one launch per step (the one-step kernel,
             # what a closed-loop caller gets), timed the same way: the A/B
@@ -854,6 +861,8 @@ def main():
         else:
             line = (multi_line if multi else optimize_line)(args, eng, world, E, S, elapsed,
                                                             kernel_ms, kernel_ms_mean, shard)
+        if 'timed_repeats' in modes:
+            line['timed_repeats_ms'] = [round(t * 1e3, 5) for t in modes['timed_repeats']]
         if 'per_step_launch' in modes:
             line['value_per_step_launch'] = world * E * args.steps / modes['per_step_launch']
             line['ms_per_step_per_step_launch'] = modes['per_step_launch'] / args.steps * 1e3

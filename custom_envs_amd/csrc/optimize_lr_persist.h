@@ -678,6 +678,9 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                     margins();
                 }
             }
+#ifdef CE_DIAG
+            if (t == 1) LP_STAMP(7);                        // step 1's row work done
+#endif
             __syncthreads();                                // partials t -> the epilogue waves
 #ifdef CE_DIAG
             if (t == 0) LP_STAMP(2);
@@ -743,6 +746,9 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
         for (int t = 0; t < m.k; ++t) {
             const int buf = t & 1;
             __syncthreads();                                // the row waves' partials of step t
+#ifdef CE_DIAG
+            if (t == 1) LP_STAMP(2);                        // epilogue waves: step 1 starts
+#endif
             if (t > 0) flush_obs(t - 1);
             const long long ro = t * m.out_step;
             if (srole) {
@@ -785,6 +791,12 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                 step_p[r] = wipe ? 0 : step_p[r] + 1;
                 rG[r] = rcp_newton2(fabs(g_prev[r]) + 1.0);
             }
+#ifdef CE_DIAG
+            if (t == 1) {                                   // step 1's epilogue issued and drained
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                LP_STAMP(7);
+            }
+#endif
         }
         __syncthreads();                                    // the last step's obs block staged
         if (m.k > 0) flush_obs(m.k - 1);

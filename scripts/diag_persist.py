@@ -5,8 +5,10 @@
 Stamps (s_memrealtime, 100 MHz chip-wide, per wave): 0 entry, 1 prologue
 loaded (state + row tiles + first actions, vmcnt(0)), 2 / 3 steps 0 / 1
 done (after their barrier), 4 step K-1's barrier, 5 loop exit, 6 final
-stores drained.  One JSON line per K: medians over waves in microseconds,
-the spread of wave starts and the launch span (first start to last drain).
+stores drained; ws form: 7 step 1's row work done (row waves) and, for the
+epilogue waves, 2 = step 1's barrier passed, 7 = step 1's epilogue
+drained.  One JSON line per K: medians over waves in microseconds, the
+spread of wave starts and the launch span (first start to last drain).
 """
 import argparse
 import ctypes
@@ -45,13 +47,14 @@ def main():
     fields, rb = eng.alloc_rollout(kmax)
     eng.reset_device({n: v[0] for n, v in fields.items() if n != '_buffer'})
     for k in args.k:
-        rows = []
+        rows, epi = [], []
         for _ in range(args.repeat):
             eng.rollout_device(k, acts, fields, rb)
             torch.cuda.synchronize()
             st = np.zeros((E, 8), np.uint64)
             _native.check(lib.ce_diag_stamps(eng._h, st.ctypes.data), 'diag')
             st = st.astype(np.int64)
+            epi.append(st[(st[:, 0] != 0) & (st[:, 1] == 0)])   # ws form: the epilogue waves
             st = st[(st[:, 0] != 0) & (st[:, 1] != 0)]    # row waves (ws form: not the epilogue waves)
             rows.append(st)
         st = np.concatenate(rows)
@@ -64,6 +67,13 @@ def main():
                'last_epilogue_us': us(st[:, 5] - st[:, 4]),
                'final_flush_drain_us': us(st[:, 6] - st[:, 5]),
                'wave_life_us': us(st[:, 6] - st[:, 0])}
+        if st[:, 7].any():      # ws form: step 1's row work and the barrier wait after it
+            res['step1_row_work_us'] = us(st[:, 7] - st[:, 2])
+            res['step1_barrier_wait_us'] = us(st[:, 3] - st[:, 7])
+        ep = np.concatenate(epi)
+        if len(ep) and ep[:, 7].any():
+            res['epilogue_waves_sampled'] = int(len(ep))
+            res['step1_epilogue_work_us'] = us(ep[:, 7] - ep[:, 2])
         last = rows[-1]
         t0 = last[:, 0].min()
         res['start_spread_us'] = float(np.percentile(last[:, 0] - t0, 99)) / 100.0
