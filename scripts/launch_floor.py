@@ -4,8 +4,8 @@
 
 For each K: the wall time of ONE rollout launch of K steps, bracketed by
 torch.cuda.synchronize() as bench.py's timed region is, median over
---repeat launches; once right after a 5-step warmup (the driver's form) and
-once after 2000 steps of back-to-back launches (the chip at its busy
+--repeat launches; once right after a 5-step warmup (the driver's form), the same after
+0.3 s of idle, and once after 2000 steps of back-to-back launches (the chip at its busy
 clock).  A least-squares line through t(K) gives the per-step slope and the
 fixed cost of one launch (host submission + dispatch + prologue + drain +
 completion signal).  Also the same bracket around a 1-element torch kernel:
@@ -60,12 +60,16 @@ def main():
     x = torch.zeros(1, device='cuda')
     res['empty_torch_kernel_us'] = statistics.median(once(lambda: x.add_(1)) for _ in range(args.repeat))
     first = {}
-    for state in ('after_warmup5', 'busy'):
+    for state in ('after_warmup5', 'after_idle', 'busy'):
         t = {}
         for k in args.k:
             vals = []
             for _ in range(args.repeat):
-                if state == 'busy':
+                if state == 'after_idle':
+                    torch.cuda.synchronize()
+                    time.sleep(0.3)                      # long idle, then the 5-step warmup
+                    runners[5 if 5 in runners else min(args.k)]()
+                elif state == 'busy':
                     for _ in range(2000 // kmax):
                         runners[kmax]()
                 else:
