@@ -790,8 +790,16 @@ def main():
         elapsed = modes[gather_mode]
     else:
         primary = run_graph
-        primary(args.warmup)
-        torch.cuda.synchronize()
+        # the W warmup steps as two launches, each waited for: the first
+        # launch-and-wait cycles of a process carry a one-time cost (5-16 us,
+        # profiles/r05n_bench20_repeats_*.json, r05k_launch_floor.json) that
+        # the warmup is there to absorb; still exactly W steps
+        for n in (args.warmup - args.warmup // 2, args.warmup // 2):
+            if n:
+                if n not in runners:
+                    runners[n] = runner(n)
+                primary(n)
+                torch.cuda.synchronize()
         elapsed = _timed(torch, dist, primary, args.steps)
         if args.repeat_timed > 0:
             modes['timed_repeats'] = [_timed(torch, dist, primary, args.steps)

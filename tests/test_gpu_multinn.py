@@ -141,7 +141,7 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
         first step's loss ratio pins the loss (below)."""
         th_o = np.asarray(env.history['weights'][0], np.float64).copy()
         g_o = np.asarray(env.history['gradients'][0], np.float64).copy()
-        l_o = float(env.history['losses'][0])
+        l_o = float(np.asarray(env.history['losses'][0], np.float64).reshape(-1)[0])
         d_g = (state_tol * np.abs(g_o).max() + 1e-7 if g_engine is None else
                float(np.abs(np.asarray(g_engine, np.float64) - g_o).max()))
         d_l = state_tol * abs(l_o) if l_engine is None else abs(float(l_engine) - l_o)
