@@ -987,7 +987,7 @@ def _traffic_bench_args(args):
     out = ['--workload', args.workload, '--envs', str(args.envs), '--profile-only',
            '--steps', str(max(k, 6)), '--warmup', str(k), '--graph-steps', str(args.graph_steps),
            '--precision', args.precision]
-    if args.workload in ('mlp', 'nn'):
+    if args.workload == 'mlp':            # the nn workload's network and batch are fixed
         out += ['--batch-size', str(args.batch_size), '--hidden', ','.join(map(str, args.hidden))]
     return out
 
