@@ -691,8 +691,9 @@ int ce_create(const ce_config *cfg, const double *features, const int32_t *label
             if ((rc = ce::net_create(&e->net, a, cfg->device)) != CE_OK) return bail(rc);
             std::string name = "net<";
             for (size_t i = 0; i < dims.size(); ++i) name += (i ? "," : "") + std::to_string(dims[i]);
-            // ":mfma": the hand-written MFMA kernels of net_kernels.h
-            e->kernel_name = name + ">:mfma";
+            // ":mfma": the hand-written MFMA kernels of net_kernels.h; ":wide":
+            // a hidden layer wider than 256, the tiled kernels of net_wide.h
+            e->kernel_name = name + (e->net_geo.wide ? ">:wide" : ">:mfma");
         }
     }
 #undef CE_TRY

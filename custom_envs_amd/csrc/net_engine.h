@@ -5,7 +5,10 @@
 // The fused config-3 kernel (mlp_kernels.h) keeps the one shape it is
 // written for (hidden 64, B = 32); every other network runs here, on the
 // hand-written MFMA kernels of net_kernels.h (the launch sequence is listed
-// there).  Limits: 1-4 hidden layers of width <= 256, K <= 32 classes.
+// there) when every hidden layer is at most 256 wide; a network with a wider
+// hidden layer runs on the wide-layer kernels of net_wide.h (a natural weight
+// image, plain tiled float32 kernels).  Limits: 1-4 hidden layers, K <= 32
+// classes.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -30,6 +33,7 @@ static_assert(kNetChunk == 16 || kNetChunk == 32, "CE_NET_CHUNK: 16 or 32");
 
 // Shape of the network and of its per-env weight IMAGE (net_kernels.h).
 struct NetGeom {
+    int wide;                        // a hidden layer > kNetMaxOp: the natural image, net_wide.h
     int nl;                          // dense layers (hidden + output)
     int din[kNetL], dout[kNetL];     // true widths
     int op[kNetL];                   // d_out padded to a multiple of 64
@@ -45,6 +49,9 @@ struct NetGeom {
     int64_t P;                       // flat parameters
 };
 
+// The natural image of the wide path: layer l's rows are its input units in
+// order (op_l columns), its biases in unit order.
+constexpr int kNetMaxWide = 8192;         // widest hidden layer of the wide path
 // Image row of input unit u of layer l.  Layer 0: the feature index.  A
 // hidden layer's input unit u = 64c + 16g + 4i + j is register i of block
 // (c, j) in lane group g of the previous layer's 16x16 accumulators; chunk

@@ -11,6 +11,7 @@
 
 #include "common.h"
 #include "net_kernels.h"
+#include "net_wide.h"
 
 namespace ce {
 
@@ -43,13 +44,36 @@ int net_geometry(int n_hidden, const int *dims, NetGeom *g) {
     g->nl = nl;
     for (int l = 0; l <= nl; ++l)
         if (dims[l] <= 0) return fail(CE_EINVAL, "network: widths must be positive");
-    for (int l = 1; l < nl; ++l)
-        if (dims[l] > kNetMaxOp)
-            return fail(CE_EUNSUPPORTED, "network: hidden widths up to " + std::to_string(kNetMaxOp) +
-                                             " (the forward keeps a layer's activations in MFMA "
-                                             "accumulators)");
+    // a hidden layer wider than the MFMA forward's accumulators hold: the
+    // wide-layer path (net_wide.h), natural image layout
+    for (int l = 1; l < nl; ++l) {
+        if (dims[l] > kNetMaxWide)
+            return fail(CE_EUNSUPPORTED, "network: hidden widths up to " + std::to_string(kNetMaxWide));
+        if (dims[l] > kNetMaxOp) g->wide = 1;
+    }
     if (dims[nl] > kNetMaxClasses)
         return fail(CE_EUNSUPPORTED, "network: at most 32 classes");
+    if (g->wide) {
+        int64_t flat = 0, img = 0;
+        int bias = 0;
+        for (int l = 0; l < nl; ++l) {
+            g->din[l] = dims[l];
+            g->dout[l] = dims[l + 1];
+            g->op[l] = round_up(dims[l + 1], 64);
+            g->nchunk[l] = (dims[l] + kNetChunk - 1) / kNetChunk;
+            g->img_off[l] = img;
+            g->bias_rel[l] = bias;
+            g->flat_w[l] = flat;
+            img += static_cast<int64_t>(dims[l]) * g->op[l];
+            bias += g->op[l];
+            flat += static_cast<int64_t>(dims[l]) * dims[l + 1] + dims[l + 1];
+        }
+        g->bias_total = bias;
+        g->bias_base = img;
+        g->Pimg = (img + bias + 63) / 64 * 64;
+        g->P = flat;
+        return CE_OK;
+    }
     // every hidden layer padded to one width (64 or 256 units): the forward
     // is compiled per hidden-layer width (net_fwd_kernel<NCGH>); the output
     // layer (K <= 32) has 64
@@ -90,10 +114,10 @@ void net_flat_to_image(const NetGeom &g, const float *flat, float *img) {
     for (int l = 0; l < g.nl; ++l) {
         const int din = g.din[l], dout = g.dout[l];
         for (int k = 0; k < din; ++k)
-            std::memcpy(img + g.img_off[l] + static_cast<int64_t>(net_img_row(l, k)) * g.op[l],
+            std::memcpy(img + g.img_off[l] + static_cast<int64_t>(g.wide ? k : net_img_row(l, k)) * g.op[l],
                         flat + g.flat_w[l] + static_cast<int64_t>(k) * dout, dout * sizeof(float));
         const float *b = flat + g.flat_w[l] + static_cast<int64_t>(din) * dout;
-        for (int u = 0; u < dout; ++u) img[g.bias_base + g.bias_rel[l] + net_bias_slot(u)] = b[u];
+        for (int u = 0; u < dout; ++u) img[g.bias_base + g.bias_rel[l] + (g.wide ? u : net_bias_slot(u))] = b[u];
     }
 }
 
@@ -102,10 +126,10 @@ void net_image_to_flat(const NetGeom &g, const float *img, float *flat) {
         const int din = g.din[l], dout = g.dout[l];
         for (int k = 0; k < din; ++k)
             std::memcpy(flat + g.flat_w[l] + static_cast<int64_t>(k) * dout,
-                        img + g.img_off[l] + static_cast<int64_t>(net_img_row(l, k)) * g.op[l],
+                        img + g.img_off[l] + static_cast<int64_t>(g.wide ? k : net_img_row(l, k)) * g.op[l],
                         dout * sizeof(float));
         float *b = flat + g.flat_w[l] + static_cast<int64_t>(din) * dout;
-        for (int u = 0; u < dout; ++u) b[u] = img[g.bias_base + g.bias_rel[l] + net_bias_slot(u)];
+        for (int u = 0; u < dout; ++u) b[u] = img[g.bias_base + g.bias_rel[l] + (g.wide ? u : net_bias_slot(u))];
     }
 }
 
@@ -130,6 +154,7 @@ struct NetPlan {
     int tpe = 0;                             // net_grad_kernel tasks per env
     int cus = 256;                           // compute units (the persistent grad grid)
     int upd_blocks = 0;
+    float *wide_buf[2] = {nullptr, nullptr}; // wide path, B < N: the info forward's layers [E][N][op_max]
 };
 
 int64_t net_params(int F, int K, int n_hidden, const int *hidden) {
@@ -178,8 +203,9 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
     const size_t E = a.E, B = a.B, N = a.N;
     if (hipSetDevice(device) != hipSuccess) return bail(fail(CE_EHIP, "network: hipSetDevice"));
     // the dataset in the forward's B-operand order: lane g*16 + n of 16-row
-    // block rb, feature group t holds X[16 rb + n][16 t + 4 g .. + 3]
-    {
+    // block rb, feature group t holds X[16 rb + n][16 t + 4 g .. + 3] (the
+    // wide path reads the rows as they are)
+    if (!geo.wide) {
         const size_t nrb = static_cast<size_t>(p->T) * (kNetTile / 16);
         std::vector<float> xt(nrb * p->F16 * 64 * 4, 0.0f);
         std::vector<float> xh(N * a.F);
@@ -199,8 +225,15 @@ int net_create(NetPlan **out, const NetArgs &a, int device) {
     if (B < N) {
         p->Tmb = (a.B + kNetTile - 1) / kNetTile;
         const size_t rows = static_cast<size_t>(p->Tmb) * kNetTile;
-        if ((rc = dev_alloc(&p->Xmb, E * rows * p->F16 * 16, true)) != CE_OK) return bail(rc);
-        if ((rc = dev_alloc(&p->label_mb, E * rows, true)) != CE_OK) return bail(rc);
+        if (!geo.wide) {     // the MFMA forward's gathered minibatch operands
+            if ((rc = dev_alloc(&p->Xmb, E * rows * p->F16 * 16, true)) != CE_OK) return bail(rc);
+            if ((rc = dev_alloc(&p->label_mb, E * rows, true)) != CE_OK) return bail(rc);
+        } else {             // the wide path's info forward, layer by layer (ping-pong)
+            int opm = 64;
+            for (int l = 0; l < geo.nl; ++l) opm = std::max(opm, geo.op[l]);
+            for (int i = 0; i < 2; ++i)
+                if ((rc = dev_alloc(&p->wide_buf[i], E * N * opm, true)) != CE_OK) return bail(rc);
+        }
         if ((rc = dev_alloc(&p->mb_loss, E * p->Tmb, true)) != CE_OK) return bail(rc);
         if ((rc = dev_alloc(&p->mb_hits, E * p->Tmb, true)) != CE_OK) return bail(rc);
     }
@@ -252,6 +285,8 @@ void net_destroy(NetPlan *p) {
         if (p->act_mb[l]) (void)hipFree(p->act_mb[l]);
         if (p->dz_mb[l]) (void)hipFree(p->dz_mb[l]);
     }
+    for (float *b : p->wide_buf)
+        if (b) (void)hipFree(b);
     delete p;
 }
 
@@ -289,10 +324,165 @@ NetFinArgs fin_args(const NetPlan *p, const NetArgs &a) {
     return f;
 }
 
+NetGradArgs grad_args(const NetPlan *p, const NetArgs &a) {
+    NetGradArgs r{};
+    r.g = p->g;
+    r.E = a.E;
+    r.N = a.N;
+    r.B = a.B;
+    r.P = a.P;
+    r.F = a.F;
+    r.max_steps = a.max_steps;
+    r.auto_reset = a.auto_reset;
+    r.tpe = p->tpe;
+    for (int l = 0; l <= kNetL; ++l) r.task0[l] = p->task0[std::min(l, p->g.nl)];
+    for (int l = 0; l < kNetL; ++l) {
+        r.ut[l] = p->ut[l];
+        r.act_mb[l] = p->act_mb[l];
+        r.dz_mb[l] = p->dz_mb[l];
+    }
+    r.X = a.X;
+    r.order = a.B < a.N ? a.order : nullptr;
+    r.order_sel = a.order_sel;
+    r.dz_out = p->dz_out;
+    r.step = a.step;
+    r.G = a.G;
+    r.obs = a.obs;
+    return r;
+}
+
+int op_max(const NetGeom &g) {
+    int m = 64;
+    for (int l = 0; l < g.nl; ++l) m = std::max(m, g.op[l]);
+    return m;
+}
+
+// The wide-layer path (net_wide.h): every launch on the caller's stream.
+int net_step_wide(NetPlan *p, const NetArgs &a, hipStream_t s) {
+    const NetGeom &g = p->g;
+    const int E = a.E, nl = g.nl, B = a.B;
+    const bool split = p->Tmb > 0;                          // B < N: a separate info forward
+    const int64_t Bs = B;
+    {
+        WideUpdArgs u{};
+        u.g = g;
+        u.E = E;
+        u.P = a.P;
+        u.img = a.W;
+        u.act = a.act;
+        u.step = a.step;
+        const unsigned bx = static_cast<unsigned>(std::min<int64_t>(256, (a.P + 255) / 256));
+        hipLaunchKernelGGL(net_wide_update_kernel, dim3(bx, E), dim3(256), 0, s, u);
+    }
+    auto gemm = [&](const WideGemmArgs &ga) {
+        const dim3 grid((ga.N + kWideTile - 1) / kWideTile, (ga.M + kWideTile - 1) / kWideTile, E);
+        hipLaunchKernelGGL(net_wide_gemm_kernel, grid, dim3(256), 0, s, ga);
+    };
+    // H_l = relu(H_{l-1} W'_l + b'_l) (the output layer: the logits)
+    auto layer_fwd = [&](int l, int R, const float *in, int64_t in_env, int ldin, bool gather, float *out,
+                         int64_t out_env) {
+        WideGemmArgs ga{};
+        ga.E = E;
+        ga.M = R;
+        ga.N = g.dout[l];
+        ga.K = g.din[l];
+        ga.A = in;
+        ga.a_env = in_env;
+        ga.lda = ldin;
+        if (gather) {
+            ga.order = a.order;
+            ga.order_sel = a.order_sel;
+            ga.n_rows = a.N;
+        }
+        ga.B = a.W + g.img_off[l];
+        ga.b_env = g.Pimg;
+        ga.ldb = g.op[l];
+        ga.bias = a.W + g.bias_base + g.bias_rel[l];
+        ga.bias_env = g.Pimg;
+        ga.relu = l + 1 < nl;
+        ga.C = out;
+        ga.c_env = out_env;
+        ga.ldc = g.op[l];
+        gemm(ga);
+    };
+    auto loss = [&](int R, int T, float *Z, int64_t z_env, bool gather, bool dz, double *pl, int32_t *ph) {
+        WideLossArgs la{};
+        la.E = E;
+        la.R = R;
+        la.K = g.dout[nl - 1];
+        la.T = T;
+        la.write_dz = dz ? 1 : 0;
+        la.Z = Z;
+        la.z_env = z_env;
+        la.ldz = g.op[nl - 1];
+        la.label = a.label;
+        if (gather) {
+            la.order = a.order;
+            la.order_sel = a.order_sel;
+            la.n_rows = a.N;
+        }
+        la.part_loss = pl;
+        la.part_hits = ph;
+        hipLaunchKernelGGL(net_wide_loss_kernel, dim3(T, E), dim3(64), 0, s, la);
+    };
+    // the minibatch forward over sequence[0] (B < N: through the env's row
+    // order; B == N: every row in order, which is also the info forward)
+    for (int l = 0; l < nl; ++l) {
+        float *out = l + 1 == nl ? p->dz_out : p->act_mb[l];
+        if (l == 0) layer_fwd(0, B, a.X, 0, a.F, split, out, Bs * g.op[0]);
+        else layer_fwd(l, B, p->act_mb[l - 1], Bs * g.op[l - 1], g.op[l - 1], false, out, Bs * g.op[l]);
+    }
+    loss(B, split ? p->Tmb : p->T, p->dz_out, Bs * g.op[nl - 1], split, true, split ? p->mb_loss : p->part_loss,
+         split ? p->mb_hits : p->part_hits);
+    if (split) {   // info['objective'] / ['accuracy'] over every dataset row at W'
+        const int64_t ne = static_cast<int64_t>(a.N) * op_max(g);
+        const float *in = a.X;
+        int64_t in_env = 0;
+        int ldin = a.F;
+        for (int l = 0; l < nl; ++l) {
+            float *out = p->wide_buf[l & 1];
+            layer_fwd(l, a.N, in, in_env, ldin, false, out, ne);
+            in = out;
+            in_env = ne;
+            ldin = g.op[l];
+        }
+        loss(a.N, p->T, p->wide_buf[(nl - 1) & 1], ne, false, false, p->part_loss, p->part_hits);
+    }
+    // dZ_l = (dZ_{l+1} W'_{l+1}^T) * (H_l > 0), top down
+    for (int lh = nl - 2; lh >= 0; --lh) {
+        const int lo = lh + 1;
+        WideGemmArgs ga{};
+        ga.E = E;
+        ga.M = B;
+        ga.N = g.dout[lh];
+        ga.K = g.dout[lo];
+        ga.A = lo == nl - 1 ? p->dz_out : p->dz_mb[lo];
+        ga.a_env = Bs * g.op[lo];
+        ga.lda = g.op[lo];
+        ga.B = a.W + g.img_off[lo];
+        ga.b_env = g.Pimg;
+        ga.ldb = g.op[lo];
+        ga.b_trans = 1;
+        ga.mask = p->act_mb[lh];
+        ga.mask_env = Bs * g.op[lh];
+        ga.ldm = g.op[lh];
+        ga.C = p->dz_mb[lh];
+        ga.c_env = Bs * g.op[lh];
+        ga.ldc = g.op[lh];
+        gemm(ga);
+    }
+    const int grid = 8 * std::min(p->tpe, kNetGradBlocks) * ((E + 7) / 8);
+    hipLaunchKernelGGL(net_grad_kernel, dim3((grid + 7) / 8 * 8), dim3(kNetThreads), 0, s, grad_args(p, a));
+    hipLaunchKernelGGL(net_finish_kernel, dim3(E), dim3(kNetThreads), 0, s, fin_args(p, a));
+    CE_HIP(hipGetLastError());
+    return CE_OK;
+}
+
 }  // namespace
 
 int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
     const NetGeom &g = p->g;
+    if (g.wide) return net_step_wide(p, a, s);
     const int E = a.E, nl = g.nl;
     const bool split = p->Tmb > 0;                          // B < N: a separate minibatch forward
     // B <= 32 (the minibatch in waves 0-1): the update rides in the minibatch
@@ -411,29 +601,7 @@ int net_step(NetPlan *p, const NetArgs &a, hipStream_t s) {
         hipLaunchKernelGGL(net_bwd_kernel, dim3(E), dim3(kNetThreads), 0, gs, b);
     }
     {
-        NetGradArgs r{};
-        r.g = g;
-        r.E = E;
-        r.N = a.N;
-        r.B = a.B;
-        r.P = a.P;
-        r.F = a.F;
-        r.max_steps = a.max_steps;
-        r.auto_reset = a.auto_reset;
-        r.tpe = p->tpe;
-        for (int l = 0; l <= kNetL; ++l) r.task0[l] = p->task0[std::min(l, nl)];
-        for (int l = 0; l < kNetL; ++l) {
-            r.ut[l] = p->ut[l];
-            r.act_mb[l] = p->act_mb[l];
-            r.dz_mb[l] = p->dz_mb[l];
-        }
-        r.X = a.X;
-        r.order = a.B < a.N ? a.order : nullptr;
-        r.order_sel = a.order_sel;
-        r.dz_out = p->dz_out;
-        r.step = a.step;
-        r.G = a.G;
-        r.obs = a.obs;
+        const NetGradArgs r = grad_args(p, a);
         // beside the forward: a fixed grid of ~0.62 workgroups per CU (one per
         // CU is what fits beside the forward's two; fewer spreads the same
         // traffic over the forward's whole run -- A/B in DESIGN 3.7); alone:

@@ -555,6 +555,43 @@ def test_network_class_counts(n_classes):
         eng.close()
 
 
+@pytest.mark.parametrize('hidden,batch_size', [((300,), 24), ((260, 300), None), ((512, 40, 33), 32)])
+def test_wide_network_against_oracle(hidden, batch_size):
+    """Hidden layers wider than 256 units (create_neural_net accepts any
+    width, utils/utils_model.py:34): the wide-layer path (net_wide.h, a
+    natural weight image, tiled float32 kernels; the gradient's float64
+    epilogue and the finish kernel shared with the MFMA path) against the
+    oracle -- a minibatch, the full batch (B = N), three hidden layers with
+    odd widths; 3 envs across an auto-reset, weights bit-equal every step."""
+    from oracle.gen_golden import mlp_dataset
+    features, targets = mlp_dataset()
+    eng = _net_engine(features, targets, 3, hidden, batch_size)
+    try:
+        assert eng.step_kernel == 'net<%s>:wide' % ','.join(map(str, (16,) + hidden + (10,)))
+        _net_check(features, targets, eng, hidden, batch_size, [21, 22, 23], 41, scale=3e-3)
+    finally:
+        eng.close()
+
+
+def test_wide_network_512_on_mnist_shape():
+    """an oracle test at width 512 -- 784 -> 512 -> 10 over the
+    MNIST-sized set (1024 x 784), B = 32, 2 envs across an auto-reset; and the
+    state round trip through the natural image (set_state / get_state)."""
+    from custom_envs_amd.data import load_data
+    seq = load_data('mnist_synthetic', batch_size=32)
+    eng = _net_engine(seq.features, seq.targets, 2, (512,), 32)
+    try:
+        assert eng.step_kernel == 'net<784,512,10>:wide'
+        _net_check(seq.features, seq.targets, eng, (512,), 32, [5, 6], 41)
+        st = eng.get_state()
+        rs = np.random.RandomState(1)
+        w = rs.normal(0, 0.05, st['weights'].shape).astype(np.float32).astype(np.float64)
+        eng.set_state(weights=w)
+        assert np.array_equal(eng.get_state()['weights'], w)
+    finally:
+        eng.close()
+
+
 def test_network_full_batch_and_depth():
     """The default network with the full batch (B = N: every row is a
     minibatch row, the info numbers are the minibatch's), and three hidden

@@ -119,13 +119,13 @@ def test_native_mlp_seeding_against_live_numpy(seed):
 
 @pytest.mark.parametrize('change', [dict(n_classes=33), dict(n_layers=5),
                                     dict(precision=_native.CE_F64),
-                                    dict(n_layers=2, hidden=(300, 64, 0, 0))])
+                                    dict(n_layers=2, hidden=(9000, 64, 0, 0))])
 def test_unsupported_mlp_shape_is_loud(change):
     """Networks the engine does not run (more than 32 classes, more than 4
-    hidden layers, a hidden layer wider than 256 -- the forward keeps a
-    layer's activations in MFMA accumulators --, float64) fail at ce_create
+    hidden layers, a hidden layer wider than 8192, float64) fail at ce_create
     before any HIP call; every other width / depth / batch size runs (the
-    fused config-3 kernel or the layered path)."""
+    fused config-3 kernel, the MFMA layered path up to 256 units per hidden
+    layer, the wide-layer path past it)."""
     lib = _native.load()
     base = dict(abi_version=_native.ABI_VERSION, problem=_native.CE_PROBLEM_MLP,
                 precision=_native.CE_F32, num_envs=1, n_rows=128, n_features=16,
