@@ -196,52 +196,6 @@ __device__ __forceinline__ void exp_neg_q(double (&a)[Q]) {
         a[i] = ldexp(q[i], static_cast<int>(static_cast<unsigned long long>(__double_as_longlong(big[i]))));
 }
 
-// e^-x for Q arguments x in [-700, 750] through a table of 2^(j/256)
-// (CE_LR_TEXP): m = rint(-256 x log2e) by the shifter, r = -x - m ln2/256 in
-// [-ln2/512, ln2/512], e^r - 1 = r + r^2/2 + r^3/6 + r^4/24 (truncation
-// |r|^5/120 < 4e-17 relative), e^-x = 2^(m >> 8) (T[m & 255] + T[m & 255] (e^r - 1)).
-// 10 f64 operations per value against exp_neg_q's 15; the table entry is an
-// LDS read under the polynomial.  T[j] is 2^(j/256) rounded to float64
-// (lr_build_image), so the result is within ~1.5 ulp (exp_neg_q: 3 ulp).
-constexpr int kLrExpTab = 256;
-template <int Q>
-__device__ __forceinline__ void exp_neg_tab(double (&a)[Q], const double *tab) {
-    constexpr double kShift = 0x1.8p52;
-    constexpr double kC = kLog2e * kLrExpTab;           // exact: power-of-two scale
-    constexpr double kH = kLn2Hi / kLrExpTab, kL = kLn2Lo / kLrExpTab;
-    double big[Q], r[Q], p[Q], t[Q];
-    int n[Q];
-#pragma unroll
-    for (int i = 0; i < Q; ++i) {
-        big[i] = fma(a[i], -kC, kShift);
-        const double m = big[i] - kShift;
-        r[i] = fma(m, -kL, fma(m, -kH, -a[i]));       // m kH exact: |m| < 2^19, kH 32 bits
-        const int lo = static_cast<int>(static_cast<unsigned>(__double_as_longlong(big[i])));
-        t[i] = tab[lo & (kLrExpTab - 1)];
-        n[i] = lo >> 8;                                 // floor(m / 256)
-    }
-#pragma unroll
-    for (int i = 0; i < Q; ++i) p[i] = fma(r[i], 1.0 / 24.0, 1.0 / 6.0);
-#pragma unroll
-    for (int i = 0; i < Q; ++i) p[i] = fma(p[i], r[i], 0.5);
-#pragma unroll
-    for (int i = 0; i < Q; ++i) p[i] = fma(p[i], r[i], 1.0);
-#pragma unroll
-    for (int i = 0; i < Q; ++i) p[i] *= r[i];
-#pragma unroll
-    for (int i = 0; i < Q; ++i) a[i] = ldexp(fma(t[i], p[i], t[i]), n[i]);
-}
-
-// The wave's LDS copy of the table (entries lane + 64 i): in-order LDS
-// within a wave, so no barrier before its first use
-__device__ __forceinline__ void lr_exp_table(const double *src, double *tab, int lane) {
-    double v[kLrExpTab / kWave];
-#pragma unroll
-    for (int i = 0; i < kLrExpTab / kWave; ++i) v[i] = src[lane + kWave * i];
-#pragma unroll
-    for (int i = 0; i < kLrExpTab / kWave; ++i) tab[lane + kWave * i] = v[i];
-}
-
 // the row loops' exponential: the table form, or exp_neg_q (CE_LR_TEXP=0)
 template <int Q>
 __device__ __forceinline__ void lr_exp_neg(double (&a)[Q], const double *tab) {

@@ -185,9 +185,9 @@ void lr_build_image(int F, int N, const double *x, const int32_t *y, double *img
         for (int r = 0; f < F && r < N; ++r) m = std::max(m, std::fabs(x[static_cast<size_t>(r) * F + f]));
         colmax[f] = m;
     }
-    // then T[j] = 2^(j/256), rounded to float64 (exp_neg_tab)
-    double *tab = colmax + kLrMaxF;
-    for (int j = 0; j < kLrExpTab; ++j) tab[j] = static_cast<double>(exp2l(static_cast<long double>(j) / kLrExpTab));
+    // then T[j] = 2^(j/256), rounded to float64 (exp_neg_tab, exp2_table.h)
+    static const double kTab[kLrExpTab] = CE_EXP2_TAB_256;
+    std::memcpy(colmax + kLrMaxF, kTab, sizeof(kTab));
 }
 
 void lr_launch_step(const StepArgs<double> &a, hipStream_t stream) {
