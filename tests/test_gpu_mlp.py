@@ -573,6 +573,20 @@ def test_wide_network_against_oracle(hidden, batch_size):
         eng.close()
 
 
+def test_wide_network_many_envs():
+    """The wide path's grids at more envs than tiles (the GEMM's z
+    dimension, the loss tiles, the grad kernel's XCD walk): 70 envs of
+    16 -> 300 -> 10, B = 24, every env against its oracle over 41 steps."""
+    from oracle.gen_golden import mlp_dataset
+    features, targets = mlp_dataset()
+    eng = _net_engine(features, targets, 70, (300,), 24)
+    try:
+        assert eng.step_kernel == 'net<16,300,10>:wide'
+        _net_check(features, targets, eng, (300,), 24, list(range(100, 170)), 41, scale=3e-3)
+    finally:
+        eng.close()
+
+
 def test_wide_network_512_on_mnist_shape():
     """an oracle test at width 512 -- 784 -> 512 -> 10 over the
     MNIST-sized set (1024 x 784), B = 32, 2 envs across an auto-reset; and the
