@@ -103,7 +103,7 @@ int main() {
     cfg.problem = CE_PROBLEM_MLP;
     cfg.precision = CE_F32;
     cfg.n_layers = 2;
-    cfg.hidden[0] = 300;                        // wider than the register-chained forward
+    cfg.hidden[0] = 9000;                       // past the wide-layer path's 8192 units
     cfg.hidden[1] = 64;
     EXPECT(ce_create(&cfg, X.data(), y.data(), &eng) == CE_EUNSUPPORTED);
     cfg.hidden[0] = 0;
