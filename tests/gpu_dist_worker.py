@@ -10,7 +10,10 @@ global arrays of every step to OUT.
         python tests/gpu_dist_worker.py OUT COMPACT(0|1) PIPELINED(0|1) [multi]
 
 ``multi``: config 5's MultiOptEngine (13 envs x 4 agents, func4, H = 5,
-max_batches = 30) instead of Optimize-v0.
+max_batches = 30) instead of Optimize-v0.  ``chunk``: the chunk schedule
+(ShardedEnvs(chunk=7): one persistent K-step launch per chunk into a slot of
+7 records, then ONE all-gather of the slot; the last chunk of 2 steps
+gathers out of place), pipelined over the two slots or serial.
 """
 import os
 import sys
@@ -27,6 +30,8 @@ def main():
     out_path, compact, pipelined = sys.argv[1], sys.argv[2] == '1', sys.argv[3] == '1'
     if len(sys.argv) > 4 and sys.argv[4] == 'multi':
         return main_multi(out_path, pipelined)
+    if len(sys.argv) > 4 and sys.argv[4] == 'chunk':
+        return main_chunk(out_path, compact, pipelined)
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
     import torch
     import torch.distributed as dist
@@ -65,6 +70,61 @@ def main():
         if not pipelined:
             collect(pending[slot])
             pending[slot] = None
+    for slot in (0, 1):
+        if pending[slot] is not None:
+            collect(pending[slot])
+    torch.cuda.synchronize()
+    if rank == 0:
+        np.savez(out_path, **{k: np.stack([got[t][k] for t in range(STEPS)]) for k in keys})
+    eng.close()
+    dist.destroy_process_group()
+    return 0
+
+
+def main_chunk(out_path, compact, pipelined, chunk=7):
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    import torch
+    import torch.distributed as dist
+    from custom_envs_amd.distributed import ShardedEnvs, shard_range
+    from custom_envs_amd.engine import OptimizeEngine
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    d = np.load(os.path.join(HERE, 'golden', 'lr_256x10.npz'))
+    lo, hi = shard_range(E, world, rank)
+    eng = OptimizeEngine(d['features'], d['targets'], num_envs=hi - lo)
+    assert eng.persistent, eng.many_kernel
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    eng.set_stream(stream.cuda_stream)
+    shard = ShardedEnvs(eng, E, rank, world, slots=2, collective=True, compact=compact, chunk=chunk)
+    shard.seed(BASE)
+    shard.reset(0)
+    acts = np.random.RandomState(8).normal(0, 0.02, (STEPS, E, 20)).astype(np.float32)
+    dacts = torch.from_numpy(np.ascontiguousarray(acts[:, lo:hi])).cuda()
+    keys = ('obs', 'done', 'episode_len', 'reward', 'objective', 'accuracy')
+    got, pending = {}, [None, None]
+
+    def collect(entry):
+        work, steps, t0 = entry
+        work.wait()
+        for i, res in enumerate(steps):
+            got[t0 + i] = {k: res[k].cpu().numpy() for k in keys}
+
+    t0, c = 0, 0
+    while t0 < STEPS:
+        k = min(chunk, STEPS - t0)
+        slot = c & 1 if pipelined else 0
+        if pending[slot] is not None:
+            collect(pending[slot])
+            pending[slot] = None
+        shard.rollout(dacts[t0:t0 + k], slot, k)
+        steps, work = shard.gather_chunk(slot, async_op=True, k=k)
+        pending[slot] = (work, steps, t0)
+        if not pipelined:
+            collect(pending[slot])
+            pending[slot] = None
+        t0 += k
+        c += 1
     for slot in (0, 1):
         if pending[slot] is not None:
             collect(pending[slot])

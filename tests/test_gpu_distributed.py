@@ -232,6 +232,47 @@ def test_world_n_on_one_gpu_matches_world_1(tmp_path, world, compact, pipelined,
         assert one['obs'].shape == (44, 37, 41) and one['done'].any()
 
 
+@pytest.mark.parametrize('world,compact,pipelined', [(2, True, True), (3, True, False), (3, False, True)])
+def test_chunk_schedule_world_n_on_one_gpu_matches_per_step(tmp_path, world, compact, pipelined):
+    """The chunk schedule with real HIP engine shards: `world`
+    rank processes on this one GPU, each running its shard of 37 envs as
+    persistent 7-step launches into a slot's records and all-gathering each
+    slot with ONE collective (the 2-step tail out of place); every step's
+    gathered global arrays must equal a 1-rank run stepping ONE launch and
+    ONE gather per step, bit for bit -- the persistent kernel, the strided
+    records and the chunk gather together are invisible in the results."""
+    import subprocess
+    import sys
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'gpu_dist_worker.py')
+
+    def run(n, out, mode, pipe):
+        with socket.socket() as s:
+            s.bind(('127.0.0.1', 0))
+            port = s.getsockname()[1]
+        procs = []
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1',
+                       MASTER_PORT=str(port), LOCAL_RANK='0')
+            procs.append(subprocess.Popen([sys.executable, worker, str(out), str(int(compact)),
+                                           str(int(pipe)), mode], env=env))
+        codes = []
+        for p in procs:
+            try:
+                codes.append(p.wait(timeout=150))
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        assert codes == [0] * n, codes
+        return np.load(out)
+
+    one = run(1, tmp_path / 'w1.npz', 'optimize', False)
+    many = run(world, tmp_path / 'wn.npz', 'chunk', pipelined)
+    for k in one.files:
+        assert np.array_equal(one[k], many[k], equal_nan=True), k
+    assert one['obs'].shape == (44, 37, 41) and one['done'].any()
+
+
 def test_bench_n_ranks_rehearsal_on_one_gpu():
     """bench.py's N-rank path end to end on a 1-GPU box (--one-gpu-rehearsal:
     2 ranks on cuda:0, the collectives on gloo, so the gathers run eager):
