@@ -797,6 +797,8 @@ def main():
         for n in (args.warmup - args.warmup // 2, args.warmup // 2):
             if n:
                 if n not in runners:
+                    if slab is None and hasattr(eng, 'prepare_many_device'):
+                        eng.prepare_many_device(n, actions, out)
                     runners[n] = runner(n)
                 primary(n)
                 torch.cuda.synchronize()
