@@ -59,6 +59,25 @@ def main():
     res = {'kernel': eng.many_kernel, 'envs': E, 'torch_stream': args.torch_stream}
     x = torch.zeros(1, device='cuda')
     res['empty_torch_kernel_us'] = statistics.median(once(lambda: x.add_(1)) for _ in range(args.repeat))
+
+    # the host side alone: the submission call (no wait), and a wait with
+    # nothing pending
+    def host_only(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        return (t1 - t0) * 1e6
+
+    def idle_sync():
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e6
+    k0 = min(args.k)
+    res['submit_call_us'] = statistics.median(host_only(runners[k0]) for _ in range(args.repeat))
+    res['idle_sync_us'] = statistics.median(idle_sync() for _ in range(args.repeat))
     first = {}
     for state in ('after_warmup5', 'after_idle', 'busy'):
         t = {}
