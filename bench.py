@@ -121,8 +121,10 @@ def nn_flops_per_env_step(dims):
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=2000)
-    p.add_argument('--warmup', type=int, default=200)
+    p.add_argument('--steps', type=int, default=2000,
+                   help='timed steps (optimize / multi: 20000 unless given)')
+    p.add_argument('--warmup', type=int, default=200,
+                   help='untimed steps first (optimize / multi: 20000 unless given)')
     p.add_argument('--envs', type=int, default=None,
                    help='envs per GPU (default 4096 optimize, 1024 multi)')
     p.add_argument('--workload', default='optimize',
@@ -157,6 +159,10 @@ def parse(argv=None):
                    help='rank 0 at N = 1: measure roofline.traffic in this run (two rocprofv3 '
                         '--pmc passes of this workload as child processes, scripts/traffic.py); '
                         'the default when rocprofv3 is on PATH')
+    p.add_argument('--timed-events', action='store_true',
+                   help='diagnostic: HIP events around every launch INSIDE the timed region '
+                        '(roofline.kernel_ms_timed_region); adds two event records per launch '
+                        'to the timed host path')
     p.add_argument('--repeat-timed', type=int, default=0,
                    help='diagnostic: after the timed region, time the same K steps R more '
                         'times (same bracket) and list them as timed_repeats_ms; value stays '
@@ -171,6 +177,19 @@ def parse(argv=None):
         args.measure_traffic = shutil.which('rocprofv3') is not None and not args.profile_only
     if args.workload == 'mnist' and '--steps' not in (argv or sys.argv):
         args.steps, args.warmup = 30, 3      # ~13 ms per step at 4096 envs
+    if args.workload in ('optimize', 'multi'):
+        # microsecond steps: 20,000 untimed steps bring the chip to its
+        # steady clock first (the timed region's kernel ran 2.53 us per step
+        # after 200, 2.26 after 20,000: profiles/r05z_*), then 20,000 timed
+        # (~50 ms); the driver's short form passes its own --steps / --warmup
+        given = argv or sys.argv
+
+        def has(flag):
+            return any(a == flag or a.startswith(flag + '=') for a in given)
+        if not has('--steps'):
+            args.steps = 20000
+        if not has('--warmup'):
+            args.warmup = 20000
     if args.envs is None:
         args.envs = {'multi': 1024, 'nn': 1024}.get(args.workload, 4096)
     return args
@@ -637,11 +656,21 @@ def main():
             return eng.many_runner(n, actions, out)
         return lambda: eng.step_many_device(n, actions, out)
 
+    timed_events = []               # --timed-events: (start, end, steps) per launch
+
     def run_graph(k):
         for n in chunks(k):
             if n not in runners:
                 runners[n] = runner(n)
-            runners[n]()
+            if record_events[0]:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), n)
+                ev[0].record(stream)
+                runners[n]()
+                ev[1].record(stream)
+                timed_events.append(ev)
+            else:
+                runners[n]()
+    record_events = [False]
 
     pending = [None, None]
     counter = [0]
@@ -796,13 +825,23 @@ def main():
         # the warmup is there to absorb; still exactly W steps
         for n in (args.warmup - args.warmup // 2, args.warmup // 2):
             if n:
-                if n not in runners:
-                    if slab is None and hasattr(eng, 'prepare_many_device'):
-                        eng.prepare_many_device(n, actions, out)
-                    runners[n] = runner(n)
+                for c in chunks(n):                         # launch sizes up to S
+                    if c not in runners:
+                        if slab is None:
+                            eng.prepare_many_device(c, actions, out)
+                        runners[c] = runner(c)
                 primary(n)
                 torch.cuda.synchronize()
+        # HIP events around every launch of the timed region itself when its
+        # launches queue back to back (4 or more: the host's two event
+        # records per launch run ahead of the GPU), or when asked
+        record_events[0] = args.timed_events or len(chunks(args.steps)) >= 4
         elapsed = _timed(torch, dist, primary, args.steps)
+        record_events[0] = False
+        if timed_events:
+            per = [a.elapsed_time(b) / n for a, b, n in timed_events]
+            modes['timed_region_kernel_ms'] = float(np.median(per))
+            modes['timed_region_kernel_ms_mean'] = float(np.mean(per))
         if args.repeat_timed > 0:
             modes['timed_repeats'] = [_timed(torch, dist, primary, args.steps)
                                       for _ in range(args.repeat_timed)]
@@ -832,6 +871,12 @@ def main():
     else:
         kernel_ms, kernel_ms_mean = launch_events(torch, stream,
                                                   lambda: eng.step_many_device(S, actions, out), S)
+    # the roofline's kernel time: the timed region's own launches where they
+    # were timed (the same kernels rocprofv3 traces in that run), else the
+    # loop above, which runs after the timed region on a warmer chip
+    warm_loop_ms = kernel_ms
+    if 'timed_region_kernel_ms' in modes:
+        kernel_ms, kernel_ms_mean = modes['timed_region_kernel_ms'], modes['timed_region_kernel_ms_mean']
     phase_ms = {}
     if mlp and rank == 0 and not eng.step_kernel.startswith('net<'):
         # each MLP kernel alone (CE_MLP_PHASES engines), same events method
@@ -871,6 +916,14 @@ def main():
         else:
             line = (multi_line if multi else optimize_line)(args, eng, world, E, S, elapsed,
                                                             kernel_ms, kernel_ms_mean, shard)
+        if 'timed_region_kernel_ms' in modes:
+            line['roofline']['kernel_ms_source'] = ('HIP events around every launch of the timed '
+                                                    'region (median / mean per step)')
+            line['roofline']['kernel_ms_warm_loop'] = warm_loop_ms
+        else:
+            line['roofline']['kernel_ms_source'] = ('HIP events around a loop of the same launches '
+                                                    'after the timed region (one launch timed: '
+                                                    'events inside it would sit on its host path)')
         if 'timed_repeats' in modes:
             line['timed_repeats_ms'] = [round(t * 1e3, 5) for t in modes['timed_repeats']]
         if 'per_step_launch' in modes:
