@@ -27,9 +27,11 @@ elif [ "${PART}" = a2 ]; then
   echo "bench rc=$rc"; summ $OUT/bench.log optimize; fatal $rc
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --repeat-timed 10 > $OUT/bench20.log 2>&1; rc=$?
   echo "bench20 rc=$rc"; summ $OUT/bench20.log optimize20; fatal $rc
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --profile-only --steps 2000 --warmup 250 > $OUT/prof.log 2>&1; rc=$?
+  # the default command itself under the tracer (its traffic passes and CPU
+  # baseline off: no nested profiler, no child processes)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-measure-traffic --no-cpu-baseline > $OUT/prof.log 2>&1; rc=$?
   echo "rocprof rc=$rc"; fatal $rc
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof20 -o run --output-format csv -- python3 bench.py --profile-only --steps 20 --warmup 5 > $OUT/prof20.log 2>&1; rc=$?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof20 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-measure-traffic --no-cpu-baseline > $OUT/prof20.log 2>&1; rc=$?
   echo "rocprof20 rc=$rc"; fatal $rc
   timeout -k 10 300 python -u scripts/launch_floor.py --k 1 5 20 40 --repeat 20 > $OUT/launch_floor.json 2> $OUT/launch_floor.err; rc=$?
   echo "floor rc=$rc"; cat $OUT/launch_floor.json; fatal $rc
