@@ -45,7 +45,7 @@ void launch_multi_step(const ce::MultiArgs &a, int, hipStream_t s) {
 }
 // K steps in one launch (multi_persist_kernel): the reference default history
 // H = 5 only (the compile-time instance the kernel needs)
-// the two-wave form (state wave + output wave); CE_MULTI_FORM=one runs the
+// the split form (state, rows and info waves); CE_MULTI_FORM=one runs the
 // one-wave form (A/B)
 bool multi_two_wave() {
     static const bool two = [] {
@@ -60,7 +60,7 @@ void launch_multi_persist(const ce::MultiArgs &a, int k, long long act_stride, l
     if (multi_two_wave()) {
         const long lanes = static_cast<long>(a.E) * ce::Group<P>::G;
         hipLaunchKernelGGL((ce::multi_persist2_kernel<P, 5>), dim3(static_cast<int>((lanes + 63) / 64)),
-                           dim3(128), 0, s, a, k, act_stride, out_step);
+                           dim3(192), 0, s, a, k, act_stride, out_step);
         return;
     }
     const size_t lds = ce::kMultiBlock / 64 * (64 / ce::Group<P>::G) * P * 3 * 5 * sizeof(float);

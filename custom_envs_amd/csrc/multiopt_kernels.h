@@ -751,25 +751,30 @@ __global__ __launch_bounds__(kMultiBlock) void multi_persist_kernel(MultiArgs a,
 
 namespace ce {
 
-// The two-wave form of multi_persist_kernel: the same 64 / G envs per
-// workgroup, their lanes mirrored in TWO waves on two SIMDs.  The STATE wave
-// runs the loop-carried chain (the update, the Rosenbrock pair, the three
-// observation ratios, the ring updates) and stages the step's observation
-// rows in LDS; the OUTPUT wave takes each step's per-lane results from LDS
-// and does everything nothing later depends on -- the observation rows'
-// copy-out, the fourteen info reductions, reward / done / length.  One wave
-// was latency-bound on the sum of both (≈1.7 us per 1024-env step); split,
-// a step costs about the longer half.  LDS hand-over double-buffered by step
-// parity behind one 128-thread barrier per step.  Same arithmetic, same
-// operation order as multi_persist_kernel: bit-identical outputs.
+// The split form of multi_persist_kernel (multi_persist2_kernel): the same
+// 64 / G envs per workgroup, their lanes mirrored in THREE waves on three
+// SIMDs.  The STATE wave runs the loop-carried chain only: the update, the
+// Rosenbrock pair, the raw history and the three observation ratios.  Two
+// waves take what no later step of that chain reads: the ROWS wave keeps the
+// adjusted history rings' observation columns and writes the observation
+// rows (staged in its own LDS rows, copied out as float4 lines); the INFO
+// wave keeps the |.| sums ring and writes the fourteen info values, reward,
+// done and length.  Measured per 1024-env step (profiles/r05aa_*, r05v_*):
+// one wave ≈1.7 us (latency-bound on the sum); state + one output wave that
+// also took the rings 1.21 us, bound by the state wave; rings moved to that
+// output wave 1.34 us, bound by it; three waves 0.82 us.  The per-lane
+// hand-over (the new ratios and the scalars the outputs need) is
+// double-buffered by step parity behind one 192-thread barrier per step.
+// Same arithmetic, same operation order as multi_persist_kernel:
+// bit-identical outputs.
 struct MultiXch {
-    double adj_g, adj_l, gsum, lsum, st_abs, reward;
-    float thn, lr, g, gp, loss;
+    double adj_g, adj_l, gsum, lsum, nsum, reward;
+    float thn, lr, g, gp, loss, nw, nl, ng;
     int s, terminal;
 };
 
 template <int P, int HC>
-__global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K, long long act_stride,
+__global__ __launch_bounds__(192) void multi_persist2_kernel(MultiArgs a, int K, long long act_stride,
                                                             long long out_step) {
 #pragma clang fp contract(off)
     constexpr int G = Group<P>::G;
@@ -777,7 +782,7 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
     constexpr int row = 3 * H;
     static_assert(HC > 0 && HC <= kMultiStageH, "compile-time history");
     constexpr int span = 64 / G * P * row;                  // floats of the workgroup's env block
-    __shared__ __attribute__((aligned(16))) float stage[2][span];
+    __shared__ __attribute__((aligned(16))) float stage[span];   // the output wave's rows
     __shared__ MultiXch xch[2][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t gt = static_cast<size_t>(blockIdx.x) * 64 + lane;   // the lane's (env, agent)
@@ -812,15 +817,6 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
             hg_v[k] = at32(a.hg, k * Eu * P + ep);
             hw_v[k] = at32(a.hw, k * Eu * P + ep);
         }
-        float ol_v[H], og_v[H], ow_v[H];
-        double sa_v[H];
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-            ol_v[j] = at32(a.ol, j * Eu + eu);
-            og_v[j] = at32(a.og, j * Eu * P + ep);
-            ow_v[j] = at32(a.ow, j * Eu * P + ep);
-            sa_v[j] = at32(a.sa, j * Eu * P + ep);
-        }
         for (int t = 0; t < K; ++t) {
             const int buf = t & 1;
             const float act_next = at32(a.act + (t + 1 < K ? (t + 1) * act_stride : 0), eu * P + r);
@@ -853,7 +849,6 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
             const float nl = static_cast<float>(clip100(adj_l) - 1.0);
             const float ng = static_cast<float>(clip100(adj_g) - 1.0);
             const double nsum = fabs(adj_w) + fabs(adj_g) + fabs(adj_l);
-            const int aslot = (s - 1) % H;
             double reward = 1.0 - adj_l;
             reward = reward < -100.0 ? -100.0 : (reward > 100.0 ? 100.0 : reward);
             bool terminal = s >= a.max_batches;
@@ -862,39 +857,21 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
                 reward -= static_cast<double>(a.max_batches - s);
             }
             const bool wipe = terminal && a.auto_reset;
-            double st_abs = 0.0;
-            const int k0 = aslot;
-            float *const lrow = stage[buf] + ((lane / G) * P + r) * row;
-#pragma unroll
-            for (int j = 0; j < H; ++j) {
-                const int kk = k0 - j >= 0 ? k0 - j : k0 - j + H;
-                float wk = ow_v[j], gk = og_v[j], lk = ol_v[j];
-                double sk = sa_v[j];
-                if (kk == 0) {
-                    wk = nw;
-                    gk = ng;
-                    lk = nl;
-                    sk = nsum;
-                }
-                st_abs += sk;
-                if (on) {
-                    lrow[kk] = wipe ? -1.0f : wk;
-                    lrow[H + kk] = wipe ? -1.0f : lk;
-                    lrow[2 * H + kk] = wipe ? -1.0f : gk;
-                }
-            }
             MultiXch &xo = xch[buf][lane];
             xo.adj_g = adj_g;
             xo.adj_l = adj_l;
             xo.gsum = gsum;
             xo.lsum = lsum;
-            xo.st_abs = st_abs;
+            xo.nsum = nsum;
             xo.reward = reward;
             xo.thn = thn;
             xo.lr = lr;
             xo.g = g;
             xo.gp = gp;
             xo.loss = loss;
+            xo.nw = nw;
+            xo.nl = nl;
+            xo.ng = ng;
             xo.s = s;
             xo.terminal = terminal ? 1 : 0;
 #pragma unroll
@@ -904,27 +881,12 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
                     hw_v[k] = thn;
                     hl_v[k] = loss;
                 }
-#pragma unroll
-            for (int j = 0; j < H; ++j)
-                if (j == aslot) {
-                    og_v[j] = ng;
-                    ow_v[j] = nw;
-                    sa_v[j] = nsum;
-                    ol_v[j] = nl;
-                }
             if (wipe) {
 #pragma unroll
                 for (int k = 0; k < kRawHist; ++k) {
                     hg_v[k] = k == 0 ? g_init : 0.0f;
                     hw_v[k] = k == 0 ? th_init : 0.0f;
                     hl_v[k] = k == 0 ? l_init : 0.0f;
-                }
-#pragma unroll
-                for (int j = 0; j < H; ++j) {
-                    og_v[j] = -1.0f;
-                    ow_v[j] = -1.0f;
-                    ol_v[j] = -1.0f;
-                    sa_v[j] = 0.0;
                 }
                 th = th_init;
                 gc = g_init;
@@ -935,7 +897,7 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
                 s_prev = s;
             }
             act = act_next;
-            __syncthreads();                                // step t's rows and results -> the output wave
+            __syncthreads();                                // step t's results -> the output wave
         }
         if (on) {
             at32(a.theta, ep) = th;
@@ -946,23 +908,64 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
                 at32(a.hw, k * Eu * P + ep) = hw_v[k];
                 if (i == 0) at32(a.hl, k * Eu + eu) = hl_v[k];
             }
-#pragma unroll
-            for (int j = 0; j < H; ++j) {
-                at32(a.og, j * Eu * P + ep) = og_v[j];
-                at32(a.ow, j * Eu * P + ep) = ow_v[j];
-                at32(a.sa, j * Eu * P + ep) = sa_v[j];
-                if (i == 0) at32(a.ol, j * Eu + eu) = ol_v[j];
-            }
             if (i == 0) at32(a.step, eu) = s_prev;
         }
-    } else {
-        // ======================= output wave =======================
+    } else if (wave == 1) {
+        // ===================== rows wave =====================
+        // the adjusted rings' observation columns and the rows
+        float ol_v[H], og_v[H], ow_v[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            ol_v[j] = at32(a.ol, j * Eu + eu);
+            og_v[j] = at32(a.og, j * Eu * P + ep);
+            ow_v[j] = at32(a.ow, j * Eu * P + ep);
+        }
+        float *const lrow = stage + ((lane / G) * P + r) * row;
         for (int t = 0; t < K; ++t) {
             const int buf = t & 1;
-            __syncthreads();                                // step t's rows and results staged
+            __syncthreads();                                // step t's results handed over
             const long long ro = t * out_step;
+            const MultiXch &xi = xch[buf][lane];
+            const int s = xi.s;
+            const bool wipe = xi.terminal != 0 && a.auto_reset;
+            const float nw = xi.nw, ng = xi.ng, nl = xi.nl;
+            const int aslot = (s - 1) % H;
+            const int k0 = aslot;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const int kk = k0 - j >= 0 ? k0 - j : k0 - j + H;
+                float wk = ow_v[j], gk = og_v[j], lk = ol_v[j];
+                if (kk == 0) {
+                    wk = nw;
+                    gk = ng;
+                    lk = nl;
+                }
+                if (on) {
+                    lrow[kk] = wipe ? -1.0f : wk;
+                    lrow[H + kk] = wipe ? -1.0f : lk;
+                    lrow[2 * H + kk] = wipe ? -1.0f : gk;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+                if (j == aslot) {
+                    og_v[j] = ng;
+                    ow_v[j] = nw;
+                    ol_v[j] = nl;
+                }
+            if (wipe) {
+#pragma unroll
+                for (int j = 0; j < H; ++j) {
+                    og_v[j] = -1.0f;
+                    ow_v[j] = -1.0f;
+                    ol_v[j] = -1.0f;
+                }
+            }
+            // the wave's own rows (in-order LDS within a wave), copied out in
+            // line order
+            __builtin_amdgcn_wave_barrier();
             {
-                const float *lds = stage[buf];
+                const float *lds = stage;
                 float *out = reinterpret_cast<float *>(reinterpret_cast<char *>(a.obs) + ro) + e_first * P * row;
                 constexpr int kV = (span / 4 + 63) / 64;
                 if ((nblk & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
@@ -984,7 +987,45 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
                     for (int q = lane; q < nblk; q += 64) out[q] = lds[q];
                 }
             }
+            __builtin_amdgcn_wave_barrier();                // rows read before the next step rewrites them
+        }
+        if (on) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                at32(a.og, j * Eu * P + ep) = og_v[j];
+                at32(a.ow, j * Eu * P + ep) = ow_v[j];
+                if (i == 0) at32(a.ol, j * Eu + eu) = ol_v[j];
+            }
+        }
+    } else {
+        // ===================== info wave =====================
+        // the |.| sums ring, the fourteen info values, reward / done / length
+        double sa_v[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) sa_v[j] = at32(a.sa, j * Eu * P + ep);
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // step t's results handed over
+            const long long ro = t * out_step;
             const MultiXch xi = xch[buf][lane];
+            const int s = xi.s;
+            const bool terminal = xi.terminal != 0;
+            const bool wipe = terminal && a.auto_reset;
+            const int aslot = (s - 1) % H;
+            double st_abs = 0.0;
+            const int k0 = aslot;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const int kk = k0 - j >= 0 ? k0 - j : k0 - j + H;
+                st_abs += kk == 0 ? xi.nsum : sa_v[j];
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+                if (j == aslot) sa_v[j] = xi.nsum;
+            if (wipe) {
+#pragma unroll
+                for (int j = 0; j < H; ++j) sa_v[j] = 0.0;
+            }
             const double thn = xi.thn, lr = xi.lr;
             auto mine = [&](double v) { return on ? v : 0.0; };
             const double wsum = group_sum<G>(mine(fabs(thn)));
@@ -994,9 +1035,8 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
             const double adjg = group_sum<G>(mine(fabs(xi.adj_g))) / P;
             const double gdiff = group_sum<G>(mine(fabs(static_cast<double>(xi.g) - static_cast<double>(xi.gp)))) / P;
             const double gsum_all = group_sum<G>(mine(xi.gsum));
-            const double st_all = group_sum<G>(mine(xi.st_abs));
+            const double st_all = group_sum<G>(mine(st_abs));
             if (on) {
-                const bool terminal = xi.terminal != 0;
                 if (i == 0) {
                     float *info = reinterpret_cast<float *>(reinterpret_cast<char *>(a.info) + ro) + eu * kMultiInfo;
                     info[0] = terminal ? xi.loss : __builtin_nanf("");
@@ -1019,6 +1059,10 @@ __global__ __launch_bounds__(128) void multi_persist2_kernel(MultiArgs a, int K,
                     static_cast<float>(xi.reward);
                 at32(reinterpret_cast<uint8_t *>(a.done) + ro, eu * P + r) = terminal ? 1 : 0;
             }
+        }
+        if (on) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) at32(a.sa, j * Eu * P + ep) = sa_v[j];
         }
     }
 }
