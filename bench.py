@@ -819,11 +819,15 @@ def main():
         elapsed = modes[gather_mode]
     else:
         primary = run_graph
-        # the W warmup steps as two launches, each waited for: the first
-        # launch-and-wait cycles of a process carry a one-time cost (5-16 us,
-        # profiles/r05n_bench20_repeats_*.json, r05k_launch_floor.json) that
-        # the warmup is there to absorb; still exactly W steps
-        for n in (args.warmup - args.warmup // 2, args.warmup // 2):
+        # the W warmup steps as waited launches -- four of one step, then
+        # the rest: the first launch-and-wait cycles of a process carry a
+        # one-time cost (5-16 us, profiles/r05n_bench20_repeats_*.json,
+        # r05k_launch_floor.json) that the warmup is there to absorb (two
+        # waited halves: 3.52-3.57 us per driver-form step, this: 3.48-3.54,
+        # r05ac_*); still exactly W steps
+        w1 = min(args.warmup, 4)
+        warm_sizes = [1] * w1 + ([args.warmup - w1] if args.warmup > w1 else [])
+        for n in warm_sizes:
             if n:
                 for c in chunks(n):                         # launch sizes up to S
                     if c not in runners:
