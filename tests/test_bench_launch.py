@@ -39,3 +39,20 @@ def test_parse_defaults():
     args = bench.parse([])
     assert args.gpus == 1 and args.envs == 4096 and args.workload == 'optimize'
     assert bench.parse(['--workload', 'multi']).envs == 1024
+
+
+def test_run_length_defaults():
+    """The microsecond-step workloads default to 20,000 warmup + 20,000 timed
+    steps (the chip's clock ramp); a given --steps /
+    --warmup (either spelling) wins; the other workloads keep theirs."""
+    sys.path.insert(0, ROOT)
+    import bench
+    a = bench.parse([])
+    assert (a.steps, a.warmup) == (20000, 20000)
+    a = bench.parse(['--steps', '20', '--warmup', '5'])
+    assert (a.steps, a.warmup) == (20, 5)
+    a = bench.parse(['--workload', 'multi', '--steps=7'])
+    assert (a.steps, a.warmup) == (7, 20000)
+    a = bench.parse(['--workload', 'mlp'])
+    assert (a.steps, a.warmup) == (2000, 200)
+
