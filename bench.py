@@ -934,7 +934,7 @@ def main():
             line['value_per_step_launch'] = world * E * args.steps / modes['per_step_launch']
             line['ms_per_step_per_step_launch'] = modes['per_step_launch'] / args.steps * 1e3
             line['roofline']['per_step_launch_kernel_ms'] = modes['per_step_launch_kernel_ms']
-        elif modes:
+        elif 'serial' in modes:                      # the gather schedules (N > 1 / --force-gather)
             units = world * E * args.steps
             line['value_gather_serial_per_step'] = units / modes['serial']
             line['value_gather_pipelined_per_step'] = units / modes['pipelined']
