@@ -86,15 +86,19 @@ constexpr double kLn2Hi = 6.93147180369123816490e-01;
 constexpr double kLn2Lo = 1.90821492927058770002e-10;
 constexpr double kLog2e = 1.44269504088896338700e+00;
 
-// e^-x for Q arguments x in [-700, 750] through a table of 2^(j/256)
-// (CE_LR_TEXP): m = rint(-256 x log2e) by the shifter, r = -x - m ln2/256 in
-// [-ln2/512, ln2/512], e^r - 1 = r + r^2/2 + r^3/6 + r^4/24 (truncation
-// |r|^5/120 < 4e-17 relative), e^-x = 2^(m >> 8) (T[m & 255] + T[m & 255] (e^r - 1)).
-// 10 f64 operations per value against exp_neg_q's 15; the table entry is an
-// LDS read under the polynomial.  T[j] is 2^(j/256) rounded to float64
-// (exp2_table.h, scripts/gen_exp2_table.py), so the result is within ~1.5
-// ulp (the degree-10 polynomial: 3 ulp).
-constexpr int kLrExpTab = 256;
+// e^-x for Q arguments x in [-700, 750] through a table of 2^(j/2048)
+// (CE_LR_TEXP): m = rint(-2048 x log2e) by the shifter, r = -x - m ln2/2048
+// in [-ln2/4096, ln2/4096], e^r - 1 = r + r^2/2 + r^3/6 (truncation r^4/24 <
+// 3.5e-17 relative), e^-x = 2^(m >> 11) (T[m & 2047] + T[m & 2047] (e^r - 1)).
+// 9 f64 operations per value against exp_neg_q's 15; the table entry is an
+// LDS read under the polynomial.  T[j] is 2^(j/2048) rounded to float64
+// (exp2_table.h, scripts/gen_exp2_table.py); the result is within 1.3 ulp
+// (tests/test_exp_table.py; the degree-10 polynomial: 3 ulp).  The 256-entry
+// table with a degree-4 polynomial it replaces measured 2 % slower on the
+// benchmark kernel (profiles/r05af_*).
+constexpr int kLrExpTab = CE_EXP2_TAB_SIZE;
+constexpr int kLrExpBits = 11;
+static_assert(kLrExpTab == 1 << kLrExpBits, "exp2_table.h size");
 template <int Q>
 __device__ __forceinline__ void exp_neg_tab(double (&a)[Q], const double *tab) {
     constexpr double kShift = 0x1.8p52;
@@ -106,15 +110,15 @@ __device__ __forceinline__ void exp_neg_tab(double (&a)[Q], const double *tab) {
     for (int i = 0; i < Q; ++i) {
         big[i] = fma(a[i], -kC, kShift);
         const double m = big[i] - kShift;
-        r[i] = fma(m, -kL, fma(m, -kH, -a[i]));       // m kH exact: |m| < 2^19, kH 32 bits
+        // the inner fma is exact: m kH is exact inside it, and -x - m kH,
+        // below 2^-12 in magnitude, has no bit under min(ulp(x), 2^-43)
+        r[i] = fma(m, -kL, fma(m, -kH, -a[i]));
         const int lo = static_cast<int>(static_cast<unsigned>(__double_as_longlong(big[i])));
         t[i] = tab[lo & (kLrExpTab - 1)];
-        n[i] = lo >> 8;                                 // floor(m / 256)
+        n[i] = lo >> kLrExpBits;                        // floor(m / 2048)
     }
 #pragma unroll
-    for (int i = 0; i < Q; ++i) p[i] = fma(r[i], 1.0 / 24.0, 1.0 / 6.0);
-#pragma unroll
-    for (int i = 0; i < Q; ++i) p[i] = fma(p[i], r[i], 0.5);
+    for (int i = 0; i < Q; ++i) p[i] = fma(r[i], 1.0 / 6.0, 0.5);
 #pragma unroll
     for (int i = 0; i < Q; ++i) p[i] = fma(p[i], r[i], 1.0);
 #pragma unroll
@@ -123,15 +127,24 @@ __device__ __forceinline__ void exp_neg_tab(double (&a)[Q], const double *tab) {
     for (int i = 0; i < Q; ++i) a[i] = ldexp(fma(t[i], p[i], t[i]), n[i]);
 }
 
-// The wave's LDS copy of the table (entries lane + 64 i): in-order LDS
-// within a wave, so no barrier before its first use
-__device__ __forceinline__ void lr_exp_table(const double *src, double *tab, int lane) {
-    double v[kLrExpTab / kWave];
+// The workgroup's LDS copy of the table, entries tid + NTHR i, loaded by its
+// NTHR threads (16 KB: one copy per workgroup, not per wave).  The loads are
+// issued first in the prologue, so the store waits on them alone (vmcnt
+// retires in order); the caller orders the store before the first lookup with
+// a workgroup barrier.
+template <int NTHR>
+struct LrExpSlice {
+    static_assert(kLrExpTab % NTHR == 0, "table split");
+    double v[kLrExpTab / NTHR];
+    __device__ __forceinline__ void load(const double *src, int tid) {
 #pragma unroll
-    for (int i = 0; i < kLrExpTab / kWave; ++i) v[i] = src[lane + kWave * i];
+        for (int i = 0; i < kLrExpTab / NTHR; ++i) v[i] = src[tid + NTHR * i];
+    }
+    __device__ __forceinline__ void store(double *tab, int tid) const {
 #pragma unroll
-    for (int i = 0; i < kLrExpTab / kWave; ++i) tab[lane + kWave * i] = v[i];
-}
+        for (int i = 0; i < kLrExpTab / NTHR; ++i) tab[tid + NTHR * i] = v[i];
+    }
+};
 
 template <typename T>
 struct MathConsts {};

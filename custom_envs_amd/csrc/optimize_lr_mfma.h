@@ -116,7 +116,7 @@ __host__ __device__ constexpr int lr_tile_doubles(int nkf) { return (nkf + 4 + 2
 //   [nkf + 5]  int32 pair: q = 2, 3
 // (layout [tile][slot][lane]; built by the engine at ce_create), then
 // kLrMaxF doubles: max over rows of |x[r][f]| (0 past F), the column maxima
-// of the |u| bound (CE_LR_NOCLAMP), then the kLrExpTab entries 2^(j/256) of
+// of the |u| bound (CE_LR_NOCLAMP), then the kLrExpTab entries 2^(j/2048) of
 // exp_neg_tab
 
 // MODE (lr_mode): 0 = one tile at a time, padding rows (label -1) masked
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
 #if CE_LR_OBS_STAGE
     __shared__ __attribute__((aligned(16))) float obs_s[kLrEnvs * (2 * P_MAX + 4)];
 #endif
-    __shared__ double tab_s[kLrWaves][CE_LR_TEXP ? kLrExpTab : 1];   // per-wave exp tables
+    __shared__ double tab_s[CE_LR_TEXP ? kLrExpTab : 1];   // the workgroup's exp table
 #ifdef CE_DIAG
     unsigned long long stamps[kStamps] = {0};
     stamps[6] = __builtin_amdgcn_s_memrealtime();
@@ -274,6 +274,11 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     //    G and W0 of parameter p of env e0 + j and that env's step counter;
     //  - role "scalar" (the last 16 threads, one per env of the group): L
     //    and the step counter.
+#if CE_LR_TEXP
+    // the exp table behind the image's column maxima, the first loads issued
+    LrExpSlice<kLrBlock> tslice;
+    tslice.load(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tid);
+#endif
     double2 wv[NKF];
     float2 av[NKF];
 #if CE_LR_NOCLAMP
@@ -315,10 +320,6 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     // the first group's tile loads right behind W and the action: the
     // G / step / L loads below are the epilogue's and may wait
     load_group(wave < ntiles ? wave : 0);              // unconditional: no merge-point vmcnt(0)
-#if CE_LR_TEXP
-    // the exp table behind the image's column maxima, into the wave's LDS copy
-    lr_exp_table(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tab_s[wave], lane);
-#endif
     const int np_ = kLrEnvs * P;
     const int pmul = (65536 + P - 1) / P;              // a.p_mul, formed here (uniform)
     int pj[PR], pp[PR], step_p[PR];
@@ -345,6 +346,9 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     const unsigned es = srole ? e0 + sj : 0;
     const double lprev = Lp[es];
     const int step_prev = stepp[es];
+#if CE_LR_TEXP
+    tslice.store(tab_s, tid);                           // waits on the table loads only
+#endif
 
 
     // ---- W' = W - a (optimize.py:74-75); forward B operand: the margin
@@ -408,6 +412,9 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     for (int r = 0; r < PR; ++r)
         if (prole[r] && step_p[r] + 1 >= a.max_steps && a.auto_reset) w_init[r] = a.W0[gi[r]];
 #endif
+#if CE_LR_TEXP
+    __syncthreads();                                    // the table, before the first lookup
+#endif
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -457,7 +464,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
                 if constexpr (decltype(clamp_c)::value) tx[i] = clamp_u(u[q0 + i]);
                 else tx[i] = u[q0 + i];
             }
-            lr_exp_neg<QC>(tx, tab_s[wave]);            // t = e^-u
+            lr_exp_neg<QC>(tx, tab_s);                  // t = e^-u
 #pragma unroll
             for (int i = 0; i < QC; ++i) post(u[q0 + i], tx[i], ys[q0 + i], qv[q0 + i]);
         }

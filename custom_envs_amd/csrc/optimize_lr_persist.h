@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
     __shared__ double red_l[2][W][kLrEnvs];                 // per-wave -log CE partials
     __shared__ double red_h[2][W][kLrEnvs];                 // per-wave hit counts
     __shared__ __attribute__((aligned(16))) float obs_s[2][kLrEnvs * OSM];
-    __shared__ double tab_s[W][CE_LR_TEXP ? kLrExpTab : 1];   // per-wave exp tables
+    __shared__ double tab_s[CE_LR_TEXP ? kLrExpTab : 1];   // the workgroup's exp table
 
 #ifdef CE_DIAG
     unsigned long long lp_st[8] = {0};
@@ -104,6 +104,11 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
     const int ntiles = (N + 15) / 16;
 
     // ---- once per launch: the state and the wave's row tiles into registers
+#if CE_LR_TEXP
+    // the exp table behind the image's column maxima, the first loads issued
+    LrExpSlice<BLK> tslice;
+    tslice.load(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tid);
+#endif
     unsigned ioff[NKF];                                     // element offset of (env c, feature 4k + h)
     double2 wv[NKF], w0v[NKF];
     float2 av[NKF];
@@ -142,9 +147,6 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
             for (int q = 0; q < 4; ++q) vmask |= (live && ys[q] >= 0 ? 1u : 0u) << (4 * i + q);
         }
     }
-#if CE_LR_TEXP
-    lr_exp_table(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tab_s[wave], lane);
-#endif
     int step_c = a.step[env_ok ? e : 0];                    // env c's counter (the wipe of wv)
     // role "parameter": index i = j P + p < 16 P, i = tid + r BLK
     const int np_ = kLrEnvs * P;
@@ -169,6 +171,10 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
     const unsigned es = srole ? e0 + sj : 0;
     double lprev = a.L[es];
     int step_s = a.step[es];
+#if CE_LR_TEXP
+    tslice.store(tab_s, tid);                               // waits on the table loads only
+    __syncthreads();
+#endif
     const double dB = static_cast<double>(B), rB = a.inv_B;
     double rL = rcp_newton2(lprev + 0.1);
 #pragma unroll
@@ -287,7 +293,7 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
                             if constexpr (decltype(clamp_c)::value) tx[j] = clamp_u(u[i][q0 + j]);
                             else tx[j] = u[i][q0 + j];
                         }
-                        lr_exp_neg<QC>(tx, tab_s[wave]);                  // t = e^-u
+                        lr_exp_neg<QC>(tx, tab_s);                  // t = e^-u
 #pragma unroll
                         for (int j = 0; j < QC; ++j) {
                             const bool valid = !PAD || ((vmask >> (4 * (g0 + i) + q0 + j)) & 1u);
@@ -464,7 +470,7 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
     __shared__ double red_h[2][W][kLrEnvs];
     __shared__ __attribute__((aligned(16))) float obs_s[2][kLrEnvs * OSM];
     __shared__ double xgs[W][TPW][4][kWave];                // gradient A operands
-    __shared__ double tab_s[W][CE_LR_TEXP ? kLrExpTab : 1];   // the row waves' exp tables
+    __shared__ double tab_s[CE_LR_TEXP ? kLrExpTab : 1];   // the row waves' exp table
 
 #ifdef CE_DIAG
     unsigned long long lp_st[8] = {0};
@@ -481,9 +487,17 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
     const int ntiles = (N + 15) / 16;
     const int nenv = E - e0 < kLrEnvs ? E - e0 : kLrEnvs;
 
-    // No workgroup barrier before the first step: a row wave's LDS tiles are
-    // its own (in-order within the wave), W0 is in its registers, and the
-    // staging buffers are the epilogue waves' alone.
+    // One workgroup barrier before the first step, for the shared exp table
+    // (CE_LR_TEXP): a row wave's LDS tiles are its own (in-order within the
+    // wave), W0 is in its registers, and the staging buffers are the
+    // epilogue waves' alone.
+#if CE_LR_TEXP
+    // the exp table behind the image's column maxima, the first loads issued:
+    // entries tid + 512 i, split over the row and the epilogue waves, one
+    // workgroup barrier (the epilogue waves' first) before the first lookup
+    LrExpSlice<BLK> tslice;
+    tslice.load(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tid);
+#endif
     if (wave < W) {
         // ======================= row waves =======================
         const int e = e0 + c;
@@ -529,10 +543,11 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                 for (int q = 0; q < 4; ++q) vmask |= (live && ys[q] >= 0 ? 1u : 0u) << (4 * i + q);
             }
         }
-#if CE_LR_TEXP
-        lr_exp_table(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tab_s[wave], lane);
-#endif
         int step_c = a.step[env_ok ? e : 0];
+#if CE_LR_TEXP
+        tslice.store(tab_s, tid);                           // waits on the table loads only
+        __syncthreads();
+#endif
         double wd[NKF];
         auto margins = [&]() {
 #pragma unroll
@@ -617,7 +632,7 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                                 if constexpr (decltype(clamp_c)::value) tx[j] = clamp_u(u[i][q0 + j]);
                                 else tx[j] = u[i][q0 + j];
                             }
-                            lr_exp_neg<QC>(tx, tab_s[wave]);
+                            lr_exp_neg<QC>(tx, tab_s);
 #pragma unroll
                             for (int j = 0; j < QC; ++j) {
                                 const bool valid = !PAD || ((vmask >> (4 * (g0 + i) + q0 + j)) & 1u);
@@ -722,10 +737,16 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
         const unsigned es = srole ? e0 + sj : 0;
         double lprev = a.L[es];
         int step_s = a.step[es];
+#if CE_LR_TEXP
+        tslice.store(tab_s, tid);
+#endif
         const double dB = static_cast<double>(B), rB = a.inv_B;
         double rL = rcp_newton2(lprev + 0.1);
 #pragma unroll
         for (int r = 0; r < PR; ++r) rG[r] = rcp_newton2(fabs(g_prev[r]) + 1.0);
+#if CE_LR_TEXP
+        __syncthreads();                                    // the row waves' table barrier
+#endif
         auto flush_obs = [&](int t) {
             float *ob = reinterpret_cast<float *>(reinterpret_cast<char *>(a.obs) + t * m.out_step) +
                         static_cast<unsigned>(e0) * OS;

@@ -185,8 +185,8 @@ void lr_build_image(int F, int N, const double *x, const int32_t *y, double *img
         for (int r = 0; f < F && r < N; ++r) m = std::max(m, std::fabs(x[static_cast<size_t>(r) * F + f]));
         colmax[f] = m;
     }
-    // then T[j] = 2^(j/256), rounded to float64 (exp_neg_tab, exp2_table.h)
-    static const double kTab[kLrExpTab] = CE_EXP2_TAB_256;
+    // then T[j] = 2^(j/2048), rounded to float64 (exp_neg_tab, exp2_table.h)
+    static const double kTab[kLrExpTab] = CE_EXP2_TAB;
     std::memcpy(colmax + kLrMaxF, kTab, sizeof(kTab));
 }
 

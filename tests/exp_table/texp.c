@@ -10,24 +10,24 @@
 
 #include "exp2_table.h"
 
-static const double kTab[256] = CE_EXP2_TAB_256;
+static const double kTab[CE_EXP2_TAB_SIZE] = CE_EXP2_TAB;
 static const double kLn2Hi = 6.93147180369123816490e-01, kLn2Lo = 1.90821492927058770002e-10,
                     kLog2e = 1.44269504088896338700e+00;
 
 static double exp_neg_tab(double a) {
-    const double kShift = 0x1.8p52, kC = kLog2e * 256, kH = kLn2Hi / 256, kL = kLn2Lo / 256;
+    const double kShift = 0x1.8p52, kC = kLog2e * CE_EXP2_TAB_SIZE,
+                 kH = kLn2Hi / CE_EXP2_TAB_SIZE, kL = kLn2Lo / CE_EXP2_TAB_SIZE;
     const double big = fma(a, -kC, kShift);
     const double m = big - kShift;
     const double r = fma(m, -kL, fma(m, -kH, -a));
     int64_t bits;
     memcpy(&bits, &big, 8);
     const int lo = (int)(uint32_t)bits;
-    const double t = kTab[lo & 255];
-    double p = fma(r, 1.0 / 24.0, 1.0 / 6.0);
-    p = fma(p, r, 0.5);
+    const double t = kTab[lo & (CE_EXP2_TAB_SIZE - 1)];
+    double p = fma(r, 1.0 / 6.0, 0.5);
     p = fma(p, r, 1.0);
     p *= r;
-    return ldexp(fma(t, p, t), lo >> 8);
+    return ldexp(fma(t, p, t), lo >> 11);   /* CE_EXP2_TAB_SIZE = 2^11 */
 }
 
 int main(void) {

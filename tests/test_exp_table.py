@@ -1,6 +1,6 @@
 """The f64 kernels' table exponential (exp_neg_tab) on the
 host: the committed table is what scripts/gen_exp2_table.py generates
-(2^(j/256) correctly rounded), and the algorithm restated in C over that
+(2^(j/2048) correctly rounded), and the algorithm restated in C over that
 table stays within 1.5 ulp of expl over [-700, 750], with e^0 == 1 exactly
 (the full-batch kernels' argmax relies on it)."""
 import os
@@ -20,7 +20,8 @@ def test_committed_table_is_the_generated_one(tmp_path):
     vals = gen_exp2_table.table()
     text = open(HEADER).read()
     assert all(v.hex() in text for v in vals)
-    assert vals[0] == 1.0 and len(vals) == 256
+    assert vals[0] == 1.0 and len(vals) == 2048
+    assert '#define CE_EXP2_TAB_SIZE 2048' in text
 
 
 @pytest.mark.skipif(shutil.which('gcc') is None, reason='needs gcc')
