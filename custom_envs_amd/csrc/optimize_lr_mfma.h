@@ -243,7 +243,14 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
 #if CE_LR_OBS_STAGE
     __shared__ __attribute__((aligned(16))) float obs_s[kLrEnvs * (2 * P_MAX + 4)];
 #endif
-    __shared__ double tab_s[CE_LR_TEXP ? kLrExpTab : 1];   // the workgroup's exp table
+#ifndef CE_LR_TAB_WAVE
+#define CE_LR_TAB_WAVE 0
+#endif
+    // the exp table: one copy per wave at 4 waves (no barrier before the
+    // first lookup), else one per workgroup
+    constexpr bool kTabWave = CE_LR_TAB_WAVE && W == 4;
+    constexpr int kTabCopies = kTabWave ? W : 1;
+    __shared__ double tab_s[kTabCopies][CE_LR_TEXP ? kLrExpTab : 1];
 #ifdef CE_DIAG
     unsigned long long stamps[kStamps] = {0};
     stamps[6] = __builtin_amdgcn_s_memrealtime();
@@ -276,8 +283,8 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     //    and the step counter.
 #if CE_LR_TEXP
     // the exp table behind the image's column maxima, the first loads issued
-    LrExpSlice<kLrBlock> tslice;
-    tslice.load(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tid);
+    LrExpSlice<kTabWave ? kWave : kLrBlock> tslice;
+    tslice.load(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, kTabWave ? lane : tid);
 #endif
     double2 wv[NKF];
     float2 av[NKF];
@@ -347,7 +354,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     const double lprev = Lp[es];
     const int step_prev = stepp[es];
 #if CE_LR_TEXP
-    tslice.store(tab_s, tid);                           // waits on the table loads only
+    tslice.store(tab_s[kTabWave ? wave : 0], kTabWave ? lane : tid);   // waits on the table loads only
 #endif
 
 
@@ -413,7 +420,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
         if (prole[r] && step_p[r] + 1 >= a.max_steps && a.auto_reset) w_init[r] = a.W0[gi[r]];
 #endif
 #if CE_LR_TEXP
-    __syncthreads();                                    // the table, before the first lookup
+    if constexpr (!kTabWave) __syncthreads();           // the table, before the first lookup
 #endif
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -464,7 +471,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
                 if constexpr (decltype(clamp_c)::value) tx[i] = clamp_u(u[q0 + i]);
                 else tx[i] = u[q0 + i];
             }
-            lr_exp_neg<QC>(tx, tab_s);                  // t = e^-u
+            lr_exp_neg<QC>(tx, tab_s[kTabWave ? wave : 0]);   // t = e^-u
 #pragma unroll
             for (int i = 0; i < QC; ++i) post(u[q0 + i], tx[i], ys[q0 + i], qv[q0 + i]);
         }

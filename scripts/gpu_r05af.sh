@@ -4,7 +4,9 @@
 # value, as a 2048-entry table would need) and additionally the 2^n scaling
 # as an integer add on the table entry's exponent (CE_LIB=texp3, no
 # v_ldexp_f64), against the shipped build; long run and driver form,
-# interleaved.
+# interleaved.  The builds came from a CE_TEXP_X switch in exp_neg_tab
+# (bit 0: drop the r^4/24 term; bit 1: the integer exponent add), removed
+# once the 2048-entry table shipped (profiles/r05af_*).
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
