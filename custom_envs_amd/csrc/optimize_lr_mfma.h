@@ -243,14 +243,10 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
 #if CE_LR_OBS_STAGE
     __shared__ __attribute__((aligned(16))) float obs_s[kLrEnvs * (2 * P_MAX + 4)];
 #endif
-#ifndef CE_LR_TAB_WAVE
-#define CE_LR_TAB_WAVE 0
-#endif
-    // the exp table: one copy per wave at 4 waves (no barrier before the
-    // first lookup), else one per workgroup
-    constexpr bool kTabWave = CE_LR_TAB_WAVE && W == 4;
-    constexpr int kTabCopies = kTabWave ? W : 1;
-    __shared__ double tab_s[kTabCopies][CE_LR_TEXP ? kLrExpTab : 1];
+    // the exp table, one copy per workgroup (one per wave at 4 waves, with no
+    // barrier before the first lookup, measured 6.5e8 -> 5.9-6.1e8 env-steps/s
+    // per-step launch, profiles/r05ai_*)
+    __shared__ double tab_s[CE_LR_TEXP ? kLrExpTab : 1];
 #ifdef CE_DIAG
     unsigned long long stamps[kStamps] = {0};
     stamps[6] = __builtin_amdgcn_s_memrealtime();
@@ -283,8 +279,8 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     //    and the step counter.
 #if CE_LR_TEXP
     // the exp table behind the image's column maxima, the first loads issued
-    LrExpSlice<kTabWave ? kWave : kLrBlock> tslice;
-    tslice.load(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, kTabWave ? lane : tid);
+    LrExpSlice<kLrBlock> tslice;
+    tslice.load(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tid);
 #endif
     double2 wv[NKF];
     float2 av[NKF];
@@ -354,7 +350,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     const double lprev = Lp[es];
     const int step_prev = stepp[es];
 #if CE_LR_TEXP
-    tslice.store(tab_s[kTabWave ? wave : 0], kTabWave ? lane : tid);   // waits on the table loads only
+    tslice.store(tab_s, tid);                           // waits on the table loads only
 #endif
 
 
@@ -420,7 +416,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
         if (prole[r] && step_p[r] + 1 >= a.max_steps && a.auto_reset) w_init[r] = a.W0[gi[r]];
 #endif
 #if CE_LR_TEXP
-    if constexpr (!kTabWave) __syncthreads();           // the table, before the first lookup
+    __syncthreads();                                    // the table, before the first lookup
 #endif
 #ifdef CE_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -471,7 +467,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
                 if constexpr (decltype(clamp_c)::value) tx[i] = clamp_u(u[q0 + i]);
                 else tx[i] = u[q0 + i];
             }
-            lr_exp_neg<QC>(tx, tab_s[kTabWave ? wave : 0]);   // t = e^-u
+            lr_exp_neg<QC>(tx, tab_s);                  // t = e^-u
 #pragma unroll
             for (int i = 0; i < QC; ++i) post(u[q0 + i], tx[i], ys[q0 + i], qv[q0 + i]);
         }

@@ -3,7 +3,8 @@
 # at 4 waves, no barrier before the first lookup (CE_LIB=tabwave, built with
 # -DCE_LR_TAB_WAVE=1), against one workgroup copy behind a barrier (default);
 # the parity tests on the variant first, then value_per_step_launch and the
-# headline, interleaved.
+# headline, interleaved.  The switch was removed after this run: the
+# per-wave copies were slower (profiles/r05ai_*).
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
