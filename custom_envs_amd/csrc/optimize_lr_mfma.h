@@ -78,10 +78,10 @@ typedef double lr_d4 __attribute__((ext_vector_type(4)));
 #ifndef CE_LR_OBS_STAGE
 #define CE_LR_OBS_STAGE 1
 #endif
-//  CE_LR_TEXP     e^-u through a 256-entry table of 2^(j/256) and a degree-4
-//                 polynomial (exp_neg_tab, 10 f64 operations per value)
-//                 instead of the degree-10 polynomial over [-ln2/2, ln2/2]
-//                 (exp_neg_q, 15): the row work is f64-pipe bound
+//  CE_LR_TEXP     e^-u through a 2048-entry table of 2^(j/2048) and a
+//                 degree-3 polynomial (exp_neg_tab, 9 f64 operations per
+//                 value) instead of the degree-10 polynomial over
+//                 [-ln2/2, ln2/2] (exp_neg_q, 15): the row work is f64-pipe bound
 #ifndef CE_LR_TEXP
 #define CE_LR_TEXP 1
 #endif
