@@ -97,6 +97,9 @@ constexpr double kLog2e = 1.44269504088896338700e+00;
 // table with a degree-4 polynomial it replaces measured 2 % slower on the
 // benchmark kernel (profiles/r05af_*).
 constexpr int kLrExpTab = CE_EXP2_TAB_SIZE;
+#ifndef CE_TEXP_PIN
+#define CE_TEXP_PIN 1
+#endif
 constexpr int kLrExpBits = 11;
 static_assert(kLrExpTab == 1 << kLrExpBits, "exp2_table.h size");
 template <int Q>
@@ -117,6 +120,11 @@ __device__ __forceinline__ void exp_neg_tab(double (&a)[Q], const double *tab) {
         t[i] = tab[lo & (kLrExpTab - 1)];
         n[i] = lo >> kLrExpBits;                        // floor(m / 2048)
     }
+#if CE_TEXP_PIN
+    // the table reads stay here, ahead of the polynomial that hides their
+    // latency (left alone the scheduler sinks them to their use)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int i = 0; i < Q; ++i) p[i] = fma(r[i], 1.0 / 6.0, 0.5);
 #pragma unroll
