@@ -764,61 +764,72 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                 const int j = i / OS, p = i - j * OS;
                 if (p < P) obs_s[0][i] = obs_s[1][i] = 0.0f;
             }
-        for (int t = 0; t < m.k; ++t) {
-            const int buf = t & 1;
-            __syncthreads();                                // the row waves' partials of step t
-#ifdef CE_DIAG
-            if (t == 1) LP_STAMP(2);                        // epilogue waves: step 1 starts
-#endif
-            if (t > 0) flush_obs(t - 1);
-            const long long ro = t * m.out_step;
-            if (srole) {
-                double lt = 0.0, ht = 0.0;
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    lt += red_l[buf][w][sj];
-                    ht += red_h[buf][w][sj];
+        // x / B: with a power-of-two B, x rB is the exact quotient that
+        // div_rcp's correction step would return (two operations fewer per
+        // division; the epilogue's f64 work shares the row waves' pipe)
+        auto epi_steps = [&](auto pow2_c) {
+            auto divB = [&](double x) {
+                if constexpr (decltype(pow2_c)::value) return x * rB;
+                else return div_rcp(x, dB, rB);
+            };
+            for (int t = 0; t < m.k; ++t) {
+                const int buf = t & 1;
+                __syncthreads();                                // the row waves' partials of step t
+    #ifdef CE_DIAG
+                if (t == 1) LP_STAMP(2);                        // epilogue waves: step 1 starts
+    #endif
+                if (t > 0) flush_obs(t - 1);
+                const long long ro = t * m.out_step;
+                if (srole) {
+                    double lt = 0.0, ht = 0.0;
+    #pragma unroll
+                    for (int w = 0; w < W; ++w) {
+                        lt += red_l[buf][w][sj];
+                        ht += red_h[buf][w][sj];
+                    }
+                    const double loss = divB(lt);
+                    const double acc = divB(ht);
+                    const double lnew = div_rcp(loss - lprev, lprev + 0.1, rL);
+                    const int cur = step_s + 1;
+                    const bool wipe = cur >= a.max_steps && a.auto_reset;
+                    if (a.reward) lr_store(reinterpret_cast<float *>(reinterpret_cast<char *>(a.reward) + ro) + es,
+                                           static_cast<float>(-loss));
+                    lr_store(reinterpret_cast<float *>(reinterpret_cast<char *>(a.objective) + ro) + es,
+                             static_cast<float>(loss));
+                    lr_store(reinterpret_cast<float *>(reinterpret_cast<char *>(a.accuracy) + ro) + es,
+                             static_cast<float>(acc));
+                    if (a.done) (reinterpret_cast<uint8_t *>(a.done) + ro)[es] = cur >= a.max_steps ? 1 : 0;
+                    lr_store(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro) + es, cur);
+                    obs_s[buf][sj * OS + P - OL] = wipe ? 0.0f : static_cast<float>(lnew);
+                    lprev = wipe ? 0.0 : lnew;
+                    step_s = wipe ? 0 : cur;
+                    rL = rcp_newton2(lprev + 0.1);
                 }
-                const double loss = div_rcp(lt, dB, rB);
-                const double acc = div_rcp(ht, dB, rB);
-                const double lnew = div_rcp(loss - lprev, lprev + 0.1, rL);
-                const int cur = step_s + 1;
-                const bool wipe = cur >= a.max_steps && a.auto_reset;
-                if (a.reward) lr_store(reinterpret_cast<float *>(reinterpret_cast<char *>(a.reward) + ro) + es,
-                                       static_cast<float>(-loss));
-                lr_store(reinterpret_cast<float *>(reinterpret_cast<char *>(a.objective) + ro) + es,
-                         static_cast<float>(loss));
-                lr_store(reinterpret_cast<float *>(reinterpret_cast<char *>(a.accuracy) + ro) + es,
-                         static_cast<float>(acc));
-                if (a.done) (reinterpret_cast<uint8_t *>(a.done) + ro)[es] = cur >= a.max_steps ? 1 : 0;
-                lr_store(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro) + es, cur);
-                obs_s[buf][sj * OS + P - OL] = wipe ? 0.0f : static_cast<float>(lnew);
-                lprev = wipe ? 0.0 : lnew;
-                step_s = wipe ? 0 : cur;
-                rL = rcp_newton2(lprev + 0.1);
+    #pragma unroll
+                for (int r = 0; r < PR; ++r) {
+                    if (!prole[r]) continue;
+                    const bool wipe = step_p[r] + 1 >= a.max_steps && a.auto_reset;
+                    const int f = pp[r] >> 1;
+                    double sf = 0.0;
+    #pragma unroll
+                    for (int w = 0; w < W; ++w) sf += red_s[buf][w][f >> 2][pj[r] + 16 * (f & 3)];
+                    const double g = divB((pp[r] & 1) ? sf : -sf);
+                    const double gnew = div_rcp(g, fabs(g_prev[r]) + 1.0, rG[r]);
+                    obs_s[buf][pj[r] * OS + P + 1 + pp[r] - OL] = wipe ? 0.0f : static_cast<float>(gnew);
+                    g_prev[r] = wipe ? 0.0 : gnew;
+                    step_p[r] = wipe ? 0 : step_p[r] + 1;
+                    rG[r] = rcp_newton2(fabs(g_prev[r]) + 1.0);
+                }
+    #ifdef CE_DIAG
+                if (t == 1) {                                   // step 1's epilogue issued and drained
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                    LP_STAMP(7);
+                }
+    #endif
             }
-#pragma unroll
-            for (int r = 0; r < PR; ++r) {
-                if (!prole[r]) continue;
-                const bool wipe = step_p[r] + 1 >= a.max_steps && a.auto_reset;
-                const int f = pp[r] >> 1;
-                double sf = 0.0;
-#pragma unroll
-                for (int w = 0; w < W; ++w) sf += red_s[buf][w][f >> 2][pj[r] + 16 * (f & 3)];
-                const double g = div_rcp((pp[r] & 1) ? sf : -sf, dB, rB);
-                const double gnew = div_rcp(g, fabs(g_prev[r]) + 1.0, rG[r]);
-                obs_s[buf][pj[r] * OS + P + 1 + pp[r] - OL] = wipe ? 0.0f : static_cast<float>(gnew);
-                g_prev[r] = wipe ? 0.0 : gnew;
-                step_p[r] = wipe ? 0 : step_p[r] + 1;
-                rG[r] = rcp_newton2(fabs(g_prev[r]) + 1.0);
-            }
-#ifdef CE_DIAG
-            if (t == 1) {                                   // step 1's epilogue issued and drained
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                LP_STAMP(7);
-            }
-#endif
-        }
+        };
+        if ((B & (B - 1)) == 0) epi_steps(std::true_type{});
+        else epi_steps(std::false_type{});
         __syncthreads();                                    // the last step's obs block staged
         if (m.k > 0) flush_obs(m.k - 1);
 #pragma unroll
