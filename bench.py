@@ -265,14 +265,23 @@ def host_info():
             'numpy': np.__version__}
 
 
-def cpu_share():
-    """Worker processes the box grants this job (16 CPUs per GPU there;
-    os.cpu_count() reports the whole machine)."""
+def affinity_cpus():
+    """CPUs this process may run on (os.cpu_count() is the whole machine)."""
     try:
-        n = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(n, 16))
+        return os.cpu_count() or 1
+
+
+def cpu_share():
+    """The per-GPU CPU share of the GPU boxes (16 CPUs per GPU there): the
+    second SubprocVecEnv leg, kept beside the full-affinity leg."""
+    return max(1, min(affinity_cpus(), 16))
+
+
+def _children_cpu():
+    ru = resource.getrusage(resource.RUSAGE_CHILDREN)
+    return ru.ru_utime + ru.ru_stime
 
 
 def _optimize_factory(features, targets, seed):
@@ -286,10 +295,12 @@ def _optimize_factory(features, targets, seed):
 
 def cpu_baseline(features, targets, envs, budget_s):
     """The reference's NumPy path restated: oracle envs under the restated
-    custom_envs.vectorize (concurrentvecenv.py:64-268), two legs:
+    custom_envs.vectorize (concurrentvecenv.py:64-268, 230-248), three legs:
     ThreadVecEnv at the GPU's env count (one thread + mp.Pipe per env, the
-    reference's configuration) and SubprocVecEnv with one process per CPU
-    of this job's share.  ``value`` is the faster leg."""
+    reference's configuration), SubprocVecEnv with one process per CPU of the
+    affinity mask and SubprocVecEnv at the 16-CPU per-GPU share.
+    Each leg reports the cores it used (its CPU time over its wall time).
+    ``value`` is the fastest leg."""
     from oracle.vectorize import SubprocVecEnv, ThreadVecEnv
     n = _raise_fd_limit(envs)
     venv = ThreadVecEnv([_optimize_factory(features, targets, i) for i in range(n)])
@@ -299,25 +310,42 @@ def cpu_baseline(features, targets, envs, budget_s):
     venv.close()
     thread = {'value': n * steps / wall, 'envs': n, 'steps': steps, 'wall_s': wall,
               'cpu_s': cpu, 'cores': max(1, int(round(cpu / wall)))}
-    p = cpu_share()
-    venv = SubprocVecEnv([_optimize_factory(features, targets, i) for i in range(p)], 'fork')
-    venv.reset()
-    acts = np.random.RandomState(0).normal(0, 0.01, (p, 20)).astype(np.float32)
-    steps, wall, _ = _time_cpu(venv, acts, budget_s)
-    venv.close()
-    sub = {'value': p * steps / wall, 'envs': p, 'steps': steps, 'wall_s': wall, 'cores': p}
-    best = max((thread, 'ThreadVecEnv'), (sub, 'SubprocVecEnv'), key=lambda x: x[0]['value'])
-    return {'value': best[0]['value'], 'unit': 'env-steps/s', 'cores': best[0]['cores'],
+
+    def subproc(p):
+        # workers' CPU time from RUSAGE_CHILDREN once they are joined: the
+        # cores the leg actually used, not the ones it was offered
+        c0 = _children_cpu()
+        venv = SubprocVecEnv([_optimize_factory(features, targets, i) for i in range(p)], 'fork')
+        venv.reset()
+        acts = np.random.RandomState(0).normal(0, 0.01, (p, 20)).astype(np.float32)
+        steps, wall, cpu = _time_cpu(venv, acts, budget_s)
+        venv.close()
+        used = _children_cpu() - c0 + cpu
+        return {'value': p * steps / wall, 'envs': p, 'steps': steps, 'wall_s': wall,
+                'cpu_s': used, 'cores': max(1, int(round(used / wall))), 'processes': p}
+
+    # SubprocVecEnv at one process per CPU of the host's affinity
+    # mask; the 16-process per-GPU share leg stays beside it
+    full_p = _raise_fd_limit(affinity_cpus())
+    full = subproc(full_p)
+    share_p = cpu_share()
+    share = subproc(share_p) if share_p != full_p else dict(full)
+    legs = {'ThreadVecEnv': thread, 'SubprocVecEnv_affinity': full, 'SubprocVecEnv_gpu_share': share}
+    best = max(legs.items(), key=lambda x: x[1]['value'])
+    return {'value': best[1]['value'], 'unit': 'env-steps/s', 'cores': best[1]['cores'],
             'kind': 'port',
-            'sample': ('%s leg (the faster of two): ThreadVecEnv %d envs x %d steps '
-                       '(1 thread + mp.Pipe per env, pickled step msgs, np.stack; %.1f s wall) '
-                       '= %.3g env-steps/s; SubprocVecEnv %d processes x %d steps (%.1f s '
-                       'wall) = %.3g env-steps/s; both over the float64 numpy oracle '
-                       'Optimize env, 256x10, B=N' % (
-                           best[1], thread['envs'], thread['steps'], thread['wall_s'],
-                           thread['value'], sub['envs'], sub['steps'], sub['wall_s'],
-                           sub['value'])),
-            'legs': {'ThreadVecEnv': thread, 'SubprocVecEnv': sub},
+            'sample': ('%s leg (the fastest of three): ThreadVecEnv %d envs x %d steps '
+                       '(1 thread + mp.Pipe per env, pickled step msgs, np.stack; %.1f s wall, '
+                       '%d cores used) = %.3g env-steps/s; SubprocVecEnv at the full affinity '
+                       'mask, %d processes x %d steps (%.1f s wall, %d cores used) = %.3g '
+                       'env-steps/s; SubprocVecEnv at the 16-CPU per-GPU share, %d processes x '
+                       '%d steps (%.1f s wall, %d cores used) = %.3g env-steps/s; all over the '
+                       'float64 numpy oracle Optimize env, 256x10, B=N' % (
+                           best[0], thread['envs'], thread['steps'], thread['wall_s'], thread['cores'],
+                           thread['value'], full['envs'], full['steps'], full['wall_s'], full['cores'],
+                           full['value'], share['envs'], share['steps'], share['wall_s'],
+                           share['cores'], share['value'])),
+            'legs': legs,
             'host': host_info()}
 
 
@@ -626,7 +654,8 @@ def main():
         # two packed buffers: the engine writes straight into them (no packing kernels)
         # the chunk schedule where the engine runs K steps per launch: each
         # slot holds K step records, gathered by ONE collective
-        chunk = (max(1, min(args.chunk_steps, args.steps))
+        # (at most S: the action tensor holds S step blocks)
+        chunk = (max(1, min(args.chunk_steps, args.steps, S))
                  if args.workload == 'optimize' and getattr(eng, 'persistent', False) else 1)
         shard = ShardedEnvs(eng, world * E, rank, world, slots=2, collective=True, chunk=chunk)
         out = shard.outs[0]

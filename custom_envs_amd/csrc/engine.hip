@@ -941,6 +941,16 @@ bool use_persist(const ce_engine *e, const ce_outputs &o) {
     return e->persist && e->persist_on && aligned16(o.obs);
 }
 
+// The persistent kernel stores the observation block as 16-B units: a
+// caller's misaligned obs is refused, never served by another form while
+// ce_step_many_kernel() names the persistent one
+int persist_obs_ok(const ce_engine *e, const ce_outputs &o) {
+    if (e->persist && e->persist_on && !aligned16(o.obs))
+        return fail(CE_EINVAL, "the persistent K-step kernel needs a 16-byte aligned obs "
+                               "(ce_set_persistent(e, 0) selects the per-step launches)");
+    return CE_OK;
+}
+
 }  // namespace
 
 int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
@@ -949,6 +959,7 @@ int ce_step_many(ce_engine *e, int32_t k, const float *actions, int64_t stride,
         const int rc = many_args_ok(e, k, actions, stride, out);
         if (rc != CE_OK) return rc;
         const ce_outputs o = out ? *out : region_view(e, e->d_out);
+        if (persist_obs_ok(e, o) != CE_OK) return CE_EINVAL;
         if (use_persist(e, o)) {
             CE_CLEAR_STALE_ERROR();
             (void)launch_persist(e, k, actions, stride, o, 0);
@@ -981,6 +992,7 @@ int ce_step_many_prepare(ce_engine *e, int32_t k, const float *actions, int64_t 
         const int rc = many_args_ok(e, k, actions, stride, out);
         if (rc != CE_OK) return rc;
         const ce_outputs o = out ? *out : region_view(e, e->d_out);
+        if (persist_obs_ok(e, o) != CE_OK) return CE_EINVAL;
         if (use_persist(e, o)) return CE_OK;
     }
     hipGraphExec_t exec;

@@ -65,6 +65,45 @@ def compact_derived(n_params, max_steps):
     return {'obs': obs, 'done': done, 'reward': reward}
 
 
+def check_rollout(spec, num_envs, k, actions, act_count, fields, record_bytes,
+                  per_step_actions=True):
+    """Validate a K-step strided call before its pointers reach the kernel
+    (``ce_step_many_strided`` / ``ce_multi_step_many_strided`` write record t
+    at ``t * record_bytes`` for t < k and read k action blocks).
+
+    ``spec``: the engine's ``output_fields()``.  Every field must be a
+    (>= k, rows, ...) view of the engine's dtype whose record stride IS
+    ``record_bytes``, each record contiguous and 16-byte aligned; the actions
+    a contiguous float32 device tensor of at least k (or 1) blocks."""
+    import torch
+    k = int(k)
+    if k < 1:
+        raise ValueError('k must be >= 1, got %d' % k)
+    if (actions.dtype != torch.float32 or not actions.is_contiguous()
+            or actions.device.type != 'cuda'):
+        raise ValueError('actions must be a contiguous float32 device tensor')
+    if actions.numel() < (k if per_step_actions else 1) * act_count:
+        raise ValueError('actions tensor too small: %d floats for %d steps of %d'
+                         % (actions.numel(), k if per_step_actions else 1, act_count))
+    for name, dtype, rows, tail in spec:
+        v = fields.get(name)
+        if v is None:
+            raise ValueError('rollout fields lack %r' % name)
+        if v.dtype != dtype or v.device.type != 'cuda':
+            raise ValueError('field %s must be a %s device tensor' % (name, dtype))
+        if tuple(v.shape[1:]) != (num_envs * rows,) + tuple(tail):
+            raise ValueError('field %s records have shape %s, the engine writes %s'
+                             % (name, tuple(v.shape[1:]), (num_envs * rows,) + tuple(tail)))
+        if v.shape[0] < k:
+            raise ValueError('field %s holds %d records, the call writes %d' % (name, v.shape[0], k))
+        if k > 1 and v.stride(0) * v.element_size() != int(record_bytes):
+            raise ValueError('record_bytes %d is not field %s\'s record stride (%d B)'
+                             % (record_bytes, name, v.stride(0) * v.element_size()))
+        if not v[0].is_contiguous() or v.data_ptr() % 16:
+            raise ValueError('field %s: every record must be contiguous and 16-byte aligned' % name)
+    return {n: v[0] for n, v in fields.items() if n != '_buffer'}
+
+
 class OptimizeEngine:
     """E Optimize-v0 environments advanced in lock step on one GPU."""
 
@@ -230,7 +269,8 @@ class OptimizeEngine:
                 for name, dtype, rows, tail in self.output_fields()}
 
     def _check_device_tensors(self, actions, out, steps=1, strided=False):
-        if actions.dtype.itemsize != 4 or not actions.is_contiguous():
+        import torch
+        if actions.dtype != torch.float32 or not actions.is_contiguous():
             raise ValueError('actions must be a contiguous float32 device tensor')
         if actions.numel() < steps * self.num_envs * self.act_dim:
             raise ValueError('actions tensor too small')
@@ -339,18 +379,22 @@ class OptimizeEngine:
     def rollout_device(self, k, actions, fields, record_bytes, per_step_actions=True):
         """k stream-ordered steps keeping every step's outputs: step t reads
         actions[t] and writes record t of ``fields`` (``alloc_rollout``)
-        (``ce_step_many_strided``).  One launch where ``persistent``."""
-        self._check_device_tensors(actions, {n: v[0] for n, v in fields.items() if n != '_buffer'},
-                                   k if per_step_actions else 1, strided=True)
+        (``ce_step_many_strided``).  One launch where ``persistent``.
+        ``fields`` must hold at least k records of ``record_bytes`` each
+        (``check_rollout``)."""
+        first = check_rollout(self.output_fields(), self.num_envs, k, actions, self.num_envs * self.act_dim,
+                              fields, record_bytes, per_step_actions)
+        self._check_device_tensors(actions, first, k if per_step_actions else 1, strided=True)
         stride = self.num_envs * self.act_dim if per_step_actions else 0
-        o = self._outputs({n: v[0] for n, v in fields.items() if n != '_buffer'})
+        o = self._outputs(first)
         check(self._lib.ce_step_many_strided(self._h, int(k), actions.data_ptr(), stride,
                                              ctypes.byref(o), int(record_bytes)),
               'ce_step_many_strided')
 
     def rollout_runner(self, k, actions, fields, record_bytes, per_step_actions=True):
         """rollout_device bound once (see many_runner)."""
-        first = {n: v[0] for n, v in fields.items() if n != '_buffer'}
+        first = check_rollout(self.output_fields(), self.num_envs, k, actions, self.num_envs * self.act_dim,
+                              fields, record_bytes, per_step_actions)
         self._check_device_tensors(actions, first, k if per_step_actions else 1, strided=True)
         stride = self.num_envs * self.act_dim if per_step_actions else 0
         o = self._outputs(first)

@@ -12,6 +12,7 @@ import numpy as np
 
 from custom_envs_amd import _native
 from custom_envs_amd._native import CeMultiConfig, CeMultiOutputs, check
+from custom_envs_amd.engine import check_rollout
 
 # problem names accepted by MultiOptLRs(problem=...): the reference's default
 # 'func' (2-D Rosenbrock, start [-1.9, 2.0], optimize_function.py:35-37) and
@@ -103,19 +104,20 @@ class MultiOptEngine:
 
     def rollout_device(self, k, actions, fields, record_bytes, per_step_actions=True):
         """k steps; step t reads actions[t] and writes record t of ``fields``
-        (ce_multi_step_many_strided)."""
-        if actions.numel() < (k if per_step_actions else 1) * self.rows or not actions.is_contiguous():
-            raise ValueError('actions must be a contiguous float32 tensor of k x E*P rows')
-        o = self._outputs({n: v[0] for n, v in fields.items() if n != '_buffer'})
+        (ce_multi_step_many_strided).  ``fields`` must hold at least k
+        records of ``record_bytes`` each (``engine.check_rollout``)."""
+        first = check_rollout(self.output_fields(), self.num_envs, k, actions, self.rows, fields,
+                              record_bytes, per_step_actions)
+        o = self._outputs(first)
         stride = self.rows if per_step_actions else 0
         self._call('step_many_strided', int(k), actions.data_ptr(), stride, ctypes.byref(o),
                    int(record_bytes))
 
     def rollout_runner(self, k, actions, fields, record_bytes, per_step_actions=True):
         """rollout_device bound once."""
-        if actions.numel() < (k if per_step_actions else 1) * self.rows or not actions.is_contiguous():
-            raise ValueError('actions must be a contiguous float32 tensor of k x E*P rows')
-        o = self._outputs({n: v[0] for n, v in fields.items() if n != '_buffer'})
+        first = check_rollout(self.output_fields(), self.num_envs, k, actions, self.rows, fields,
+                              record_bytes, per_step_actions)
+        o = self._outputs(first)
         fn, h, ap, ref = self._fn('step_many_strided'), self._h, actions.data_ptr(), ctypes.byref(o)
         kk, stride, rb = int(k), (self.rows if per_step_actions else 0), int(record_bytes)
 

@@ -231,7 +231,10 @@ int ce_step_many_strided(ce_engine *eng, int32_t k, const float *actions,
                          int64_t out_step_bytes);
 /* on = 1 (default; CE_PERSIST=0 in the environment at ce_create makes it 0):
  * ce_step_many and ce_step_many_strided use the persistent K-step kernel where
- * the engine has one; on = 0: one launch per step (the A/B form). */
+ * the engine has one; on = 0: one launch per step (the A/B form).  With the
+ * persistent kernel selected, every K-step entry (ce_step_many, _prepare,
+ * _strided) refuses an obs that is not 16-byte aligned with CE_EINVAL: the
+ * kernel ce_step_many_kernel names is the one that runs, or none. */
 int ce_set_persistent(ce_engine *eng, int32_t on);
 /* The kernel ce_step_many runs: "optimize_lr_persist_kernel<NKF,TPW,PAD>" when
  * persistent, else ce_step_kernel's name. */

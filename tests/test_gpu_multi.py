@@ -446,3 +446,71 @@ def test_persistent_multi_against_oracle():
         assert st['step'][e] == runner._environment.current_step
         if st['step'][e]:
             assert np.array_equal(st['theta'][e], runner._environment.model.params)
+
+
+def test_config5_global_size_on_one_engine():
+    """Config 5's GLOBAL batch as one engine: 8192 envs x 4 agents (32,768
+    agent rows; multioptlrs.py:80-129 under optvecenv.py:57-91) on the
+    persistent kernel the bench runs, with the bench's uniform(1, 3) actions
+    (the loss > 1e4 stop fires).  Envs 0, 1, 4095, 4096, 8190 and 8191
+    against live oracle runners over 48 steps in launches of 20, 20, 8:
+    every step's rows, reward, done, length and info, then theta and step."""
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    E, P, H, MB, T = 8192, 4, 5, 400, 48
+    sample = [0, 1, 4095, 4096, 8190, 8191]
+    actions = np.random.RandomState(8192).uniform(1, 3, (T, E * P)).astype(np.float32)
+    eng = MultiOptEngine(E, 'func4', max_batches=MB, max_history=H)
+    assert eng.many_kernel == 'multi_persist2_kernel<4,5>'
+    got, st = _multi_rollout(eng, actions, [20, 20, 8])
+    eng.close()
+    refs = [OptEnvRunner(OracleMulti(P, max_batches=MB, max_history=H)) for _ in sample]
+    for r in refs:
+        r.reset()
+    early = 0
+    for t in range(T):
+        for e, runner in zip(sample, refs):
+            states, rewards, dones, infos = runner.step(list(actions[t, e * P:(e + 1) * P].reshape(P, 1)))
+            grad_abs = np.abs(runner._environment.history['gradients']).astype(np.float64)
+            if dones[0]:
+                early += infos[0]['episode']['l'] < MB
+                states = runner.reset()
+            rows = slice(e * P, (e + 1) * P)
+            what = (t, e)
+            assert np.all(got['done'][t, rows] == dones[0]), what
+            assert int(got['episode_len'][t, e]) == infos[0]['episode']['l'], what
+            _close_rows(got['obs'][t, rows], np.stack(states))
+            assert abs(got['reward'][t, e * P] - rewards[0]) <= 1e-6 * max(1.0, abs(rewards[0])), what
+            _close_info(got['info'][t, e], _ref_info(infos[0]), grad_abs=grad_abs)
+    assert early > 0              # the loss > 1e4 branch was exercised
+    for e, runner in zip(sample, refs):
+        assert st['step'][e] == runner._environment.current_step
+        if st['step'][e]:
+            assert np.array_equal(st['theta'][e], runner._environment.model.params)
+
+
+def test_multi_rollout_argument_checks():
+    """The strided K-step call's host checks (engine.check_rollout): records
+    fewer than k, a record_bytes that is not the slab's stride, float64 or
+    too few actions -- all refused before any pointer reaches the kernel."""
+    import torch
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    eng = MultiOptEngine(16, 'func4', max_batches=30)
+    try:
+        fields, rb = eng.alloc_rollout(4)
+        eng.reset_device({k: v[0] for k, v in fields.items() if k != '_buffer'})
+        acts = torch.full((4, eng.rows), 2.0, device='cuda')
+        with pytest.raises(ValueError, match='holds 4 records'):
+            eng.rollout_device(5, torch.full((5, eng.rows), 2.0, device='cuda'), fields, rb)
+        with pytest.raises(ValueError, match='holds 4 records'):
+            eng.rollout_runner(50, torch.full((50, eng.rows), 2.0, device='cuda'), fields, rb)
+        with pytest.raises(ValueError, match='record stride'):
+            eng.rollout_device(4, acts, fields, rb + 256)
+        with pytest.raises(ValueError, match='float32'):
+            eng.rollout_device(4, acts.double(), fields, rb)
+        with pytest.raises(ValueError, match='too small'):
+            eng.rollout_device(4, acts[:3], fields, rb)
+        eng.rollout_device(4, acts, fields, rb)
+        eng.wait()
+        assert fields['episode_len'][:, 0].cpu().tolist() == [1, 2, 3, 4]
+    finally:
+        eng.close()

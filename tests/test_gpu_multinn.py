@@ -118,9 +118,10 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
     compared by norm, and the worst row error seen."""
     if stats is None:
         stats = {}
-    for key in ('adj_grad', 'adj_grad_finite', 'entries', 'rows'):
+    for key in ('adj_grad', 'adj_grad_finite', 'entries', 'rows', 'row_steps'):
         stats.setdefault(key, 0)
     stats.setdefault('row_err_max', 0.0)
+    rows0, slots0 = stats['rows'], stats.get('row_slots', 0)
     P = rows.size
     agent_row = np.empty(P, np.int64)
     agent_row[rows] = np.arange(P)
@@ -217,6 +218,8 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
                 snaps[0]['d_l'] = abs(l0_e - abs(snaps[0]['l'])) + 2.0 ** -22 * abs(snaps[0]['l'])
         # ---- observation parity with the oracle's rows: every column, every age
         rows_o = _oracle_rows(obs_o, names)
+        stats['row_steps'] += 1
+        stats['row_slots'] = stats.get('row_slots', 0) + P
         well = np.ones(P, bool)
         n_age = len(snaps) - 1                   # ages with a ratio this episode
         for k in range(H):
@@ -276,6 +279,12 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
         assert float(step['info'][i, 5]) == pytest.approx(lr.std(), rel=1e-4, abs=1e-9)
         ring.append(obs.copy())
         theta_prev, g_prev, l_prev = theta_after, g_e.astype(np.float64), loss
+    # the per-row 1e-5 norm bound above is not vacuous for this env: it
+    # covered at least a twentieth of the (step, row) slots compared
+    n_rows, n_slots = stats['rows'] - rows0, stats.get('row_slots', 0) - slots0
+    print('nn env %d per-row check: %d of %d (step, row) slots, worst %.3g'
+          % (i, n_rows, n_slots, stats['row_err_max']))
+    assert n_rows >= n_slots // 20, (i, n_rows, n_slots)
 
 
 def _actions(T, E, P, lo, hi, seed):
@@ -435,7 +444,12 @@ def test_default_network_benchmark_size_sampled_envs():
     stats = {}
     for k, e in enumerate(sample):
         _check_env(ds, hidden, e, acts_s[:, k], rows, rec, k, 400, stats=stats)
+    print('nn per-row check:', {k: stats[k] for k in ('rows', 'row_steps', 'row_slots', 'row_err_max')})
     assert stats['adj_grad'] >= 2 * (T - 2)
+    # the per-row 1e-5 norm bound is not vacuous: it covers at least a
+    # twentieth of all (step, row) slots compared (measured r06: NN_ROWS_SEEN)
+    assert stats['row_steps'] >= 2 * (T - 2)
+    assert stats['rows'] >= stats['row_slots'] // 20, stats
 
 
 def test_divergence_stops_early_with_penalty():

@@ -243,9 +243,52 @@ def test_strided_argument_checks(lr_dataset):
     fields, rb = eng.alloc_rollout(4)
     eng.reset_device({k: v[0] for k, v in fields.items() if k != '_buffer'})
     acts = torch.zeros((4, 64, 20), device='cuda')
-    with pytest.raises(NativeEngineError, match='multiple of 16'):
+    # the host checks (engine.check_rollout) before any pointer reaches the kernel
+    with pytest.raises(ValueError, match='record stride'):
         eng.rollout_device(4, acts, fields, rb + 4)
+    with pytest.raises(ValueError, match='holds 4 records'):
+        eng.rollout_device(5, torch.zeros((5, 64, 20), device='cuda'), fields, rb)
+    with pytest.raises(ValueError, match='holds 4 records'):
+        eng.rollout_runner(50, torch.zeros((50, 64, 20), device='cuda'), fields, rb)
+    with pytest.raises(ValueError, match='float32'):
+        eng.rollout_device(4, acts.double(), fields, rb)
+    with pytest.raises(ValueError, match='too small'):
+        eng.rollout_device(4, acts[:3], fields, rb)
+    # the native check behind it: a record stride that is not a multiple of 16
+    o = eng._outputs({k: v[0] for k, v in fields.items() if k != '_buffer'})
+    import ctypes
+    rc = eng._lib.ce_step_many_strided(eng._h, 4, acts.data_ptr(), 64 * 20, ctypes.byref(o), rb + 4)
+    assert rc != 0 and 'multiple of 16' in eng._lib.ce_last_error().decode()
     eng.rollout_device(4, acts, fields, rb)
     eng.wait()
     assert fields['episode_len'][:, 0].cpu().tolist() == [1, 2, 3, 4]
+    eng.close()
+
+
+def test_misaligned_obs_is_refused_not_rerouted(lr_dataset):
+    """with the persistent kernel selected, a caller obs that is
+    not 16-byte aligned is refused (CE_EINVAL) by every K-step entry instead
+    of silently running the per-step graph under the persistent kernel's
+    name; with ce_set_persistent(0) the per-step form takes it."""
+    import torch
+    from custom_envs_amd import NativeEngineError
+    E = 32
+    eng = _engine(lr_dataset, E)
+    eng.seed(0)
+    out = eng.alloc_device_outputs()
+    eng.reset_device(out)
+    raw = torch.zeros(E * eng.obs_dim + 1, dtype=torch.float32, device='cuda')
+    bad = dict(out, obs=raw[1:].view(E, eng.obs_dim))
+    assert bad['obs'].data_ptr() % 16 != 0
+    acts = torch.zeros((3, E, 20), device='cuda')
+    assert eng.persistent
+    with pytest.raises(NativeEngineError, match='16-byte aligned'):
+        eng.step_many_device(3, acts, bad)
+    with pytest.raises(NativeEngineError, match='16-byte aligned'):
+        eng.prepare_many_device(3, acts, bad)
+    eng.set_persistent(False)
+    assert not eng.persistent
+    eng.step_many_device(3, acts, bad)
+    eng.wait()
+    assert int(bad['episode_len'][0]) == 3
     eng.close()
