@@ -11,6 +11,8 @@ LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd.so')
 # CE_LIB=diag selects the phase-stamped profiling build (same ABI + ce_diag_stamps)
 # CE_LIB=<name> selects lib/libcustom_envs_amd_<name>.so (experiment builds).
 if os.environ.get('CE_LIB') == 'diag':
+    # never pushed to the GPU box (.gpurunignore): built there from the
+    # sources, so a stale diagnostic library cannot load
     LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd_diag.so')
 elif os.environ.get('CE_LIB'):
     LIB_PATH = os.path.join(_HERE, 'lib', 'libcustom_envs_amd_%s.so' % os.environ['CE_LIB'])
@@ -170,6 +172,9 @@ def load():
     """Load the in-tree engine library (no fallback)."""
     global _lib
     if _lib is None:
+        if os.environ.get('CE_LIB') == 'diag':
+            from custom_envs_amd import build as _build
+            _build.build(diag=True)          # rebuilt unless newer than every source
         if not os.path.exists(LIB_PATH):
             raise NativeEngineError(
                 'HIP engine library not built: %s (run python -m custom_envs_amd.build)'

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Per-env f64 MFMA kernel (optimize_mfma_kernel, CE_GEN_CAT=0) at the mnist
+# image shape: A/B of experiment builds (VARIANTS, CE_LIB; "main" = the
+# product library), interleaved twice, 4096 envs.
+set -u
+cd "$(dirname "$0")/../.."
+OUT=${OUT:-gpurun_out/gen_ab}
+mkdir -p $OUT
+export TMPDIR=/tmp CE_GEN_CAT=0
+fatal() { case $1 in 0) ;; *) echo "GPU step failed (rc=$1), stopping"; exit $1;; esac; }
+for rep in 1 2; do
+  for V in ${VARIANTS:-main}; do
+    if [ $V = main ]; then L=""; else L=$V; fi
+    CE_LIB=$L timeout -k 10 300 python bench.py --workload mnist --steps 20 --warmup 2 --no-cpu-baseline > $OUT/b_$V.log 2>&1; rc=$?
+    echo "== $V rep $rep: $(tail -1 $OUT/b_$V.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print("%.4g env-steps/s, %.3f ms/step, %s" % (d["value"], d["ms_per_step"], d["roofline"]["kernel"]))')"; fatal $rc
+  done
+done
+echo ALL_OK
