@@ -1147,6 +1147,13 @@ def optimize_line(args, eng, world, E, S, elapsed, kernel_ms, kernel_ms_mean, sh
                         'every step kept: [%d]-record slots, all-gathered' % shard.chunk
                         if shard is not None and shard.chunk > 1 else
                         'every step into the same output buffers'),
+            # say which stepping contract `value` measures
+            'stepping': ('open-loop rollout: the actions of all %d steps of a launch are '
+                         'on the device before it starts (ce_step_many_strided); a '
+                         'closed-loop caller (step t+1 chosen from step t\'s obs) gets '
+                         'value_per_step_launch' % (S if persistent else 1)
+                         if persistent else
+                         'one launch per step (the closed-loop contract of VecEnv.step)'),
             'parallelism': 'env-sharded x%d (no collective)' % world
             if shard is None else
             ('env-sharded x%d; chunks of %d steps: one persistent launch, then ONE RCCL '

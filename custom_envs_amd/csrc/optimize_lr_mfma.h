@@ -207,6 +207,17 @@ __device__ __forceinline__ void lr_exp_neg(double (&a)[Q], const double *tab) {
 #endif
 }
 
+// The argmax hit of a row by the sign bit of u (two integer operations per
+// row instead of an f64 compare and a carry add): u > 0 and "sign clear"
+// differ only at u = +0, a tie (|u| < 2^-52) that the exact re-walk after the
+// row loop settles with lr_hit, the same test.  lr_miss is 1 for a row that
+// is not a hit or not a real row (a padding row); hits = rows - misses.
+__device__ __forceinline__ unsigned lr_miss(double u, bool valid) {
+    const unsigned hi = static_cast<unsigned>(static_cast<unsigned long long>(__double_as_longlong(u)) >> 32);
+    return valid ? hi >> 31 : 1u;
+}
+__device__ __forceinline__ int lr_hit(double u) { return __double_as_longlong(u) >= 0 ? 1 : 0; }
+
 // sum of an int over lanes l, l^16, l^32, l^48 (permlane swaps)
 __device__ __forceinline__ int fold_env_lanes(int v) {
     unsigned x = static_cast<unsigned>(v), y = x;
@@ -423,13 +434,13 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
 #endif
     CE_STAMP(1);
 
-    // one gradient accumulator per tile of a group: the tiles' MFMA chains do
-    // not wait on each other (summed after the loop)
-    lr_d4 sacc[NT];
-#pragma unroll
-    for (int i = 0; i < NT; ++i) sacc[i] = lr_d4{0.0, 0.0, 0.0, 0.0};
+    // ONE gradient accumulator chain over the wave's tiles in tile order (the
+    // K-step kernels' order): each tile's MFMAs wait on the previous tile's
+    // behind its softmax anyway, and no per-tile sums are left to add
+    lr_d4 sacc = {0.0, 0.0, 0.0, 0.0};
     double prod = 1.0, nlog = 0.0, umin = 1.0;
-    int hits = 0;
+    unsigned miss = 0;
+    int rows_seen = 0;
     int since = 0;
     // two-class softmax of TwoClassModel per (row, env) in its signed form:
     // u = s_y z, t = e^-u, p_y = 1/(1+t), q = 1 - p_y = t p_y (the gradient
@@ -456,7 +467,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
             const double au = valid ? uq : 1.0;
             asm("v_min_f64 %0, %1, |%2|" : "=v"(umin) : "v"(umin), "v"(au));
         }
-        hits += (valid && uq > 0.0) ? 1 : 0;
+        miss += lr_miss(uq, valid);
     };
     auto softmax = [&](auto clamp_c, const lr_d4 &u, const int (&ys)[4], double (&qv)[4]) {
 #pragma unroll
@@ -495,7 +506,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) gv[q] = x[(h + 4 * q) * XS + cc];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sacc[slot] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[q], qv[q], sacc[slot], 0, 0, 0);
+        for (int q = 0; q < 4; ++q) sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[q], qv[q], sacc, 0, 0, 0);
         __builtin_amdgcn_wave_barrier();
     };
     // With two waves per SIMD, waves kLrWaves/2.. share SIMDs with the
@@ -513,6 +524,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     auto row_loop = [&](auto clamp_c) {
     for (int t = t_first; t < ntiles; t += NT * kLrWaves) {
         since += NT;
+        rows_seen += 4 * NT;
         if (since > 4) {                                // 16 factors in (1e-16, 1]: fold
             nlog -= log_pos(prod);
             prod = 1.0;
@@ -552,6 +564,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     // a tie (p0 == p1) is np.argmax's class 0: hit iff y == 0.  Only a wave
     // that saw |u| < 2^-52 re-walks its tiles with the exact test e^-|u| == 1
     // (practically never).
+    int hits = rows_seen - static_cast<int>(miss);
     if (__any(umin < 0x1p-52)) {
         for (int t = wave; t < ntiles; t += kLrWaves) {
             double fv[NKF];
@@ -564,7 +577,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
             exp_neg_multi_clamped<4>(tx);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                if (yv[q] >= 0 && tx[q] == 1.0) hits += (yv[q] == 0 ? 1 : 0) - (uu[q] > 0.0 ? 1 : 0);
+                if (yv[q] >= 0 && tx[q] == 1.0) hits += (yv[q] == 0 ? 1 : 0) - lr_hit(uu[q]);
         }
     }
 #if CE_LR_W0_LAZY
@@ -595,12 +608,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     lsum = fold_pair<32>(lsum, lsum);
     const double hsum = static_cast<double>(fold_env_lanes(hits));
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        double v = sacc[0][r];
-#pragma unroll
-        for (int i = 1; i < NT; ++i) v += sacc[i][r];
-        red_s[wave][r][lane] = v;
-    }
+    for (int r = 0; r < 4; ++r) red_s[wave][r][lane] = sacc[r];
     if (lane < kLrEnvs) {
         red_l[wave][lane] = lsum;
         red_h[wave][lane] = hsum;

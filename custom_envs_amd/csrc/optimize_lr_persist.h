@@ -44,6 +44,21 @@ struct ManyArgs {
 constexpr int kLpWaves = 4;                   // default: one wave per SIMD (the one-step kernel's W = 4)
 constexpr int kLpMaxTpw = 8;                  // row tiles a wave keeps in registers
 
+// The gradient on v_mfma_f64_4x4x4f64 (4 blocks of 4x4x4: feature groups of
+// 4 instead of 16 rows of M, 10 features in 12 instead of 16) where the
+// feature groups are at most 3: 4 NKF of its ~0.26-time MFMAs per 4 rows
+// against one 16x16x4 (CE_LP_G4=0 keeps the 16x16x4 form)
+#ifndef CE_LP_G4
+#define CE_LP_G4 1
+#endif
+#ifndef CE_LP_EPI_SLEEP
+#define CE_LP_EPI_SLEEP 0
+#endif
+#ifndef CE_LP_ROW_PRIO
+#define CE_LP_ROW_PRIO 3
+#endif
+__host__ __device__ constexpr bool lp_g4(int nkf) { return CE_LP_G4 && nkf <= 3; }
+
 // Row tiles per wave for N rows over W waves: the smallest of 1, 2, 4, 8
 // covering the tiles; 0 when N needs more (the caller then launches step by
 // step).
@@ -253,11 +268,9 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
 #endif
         // ---- the row work: per group of NG tiles every forward chain, then
         // per tile the signed two-class softmax and its 4 gradient MFMAs
-        lr_d4 sacc[TPW];
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) sacc[i] = lr_d4{0.0, 0.0, 0.0, 0.0};
+        lr_d4 sacc = {0.0, 0.0, 0.0, 0.0};                 // one gradient chain, tile order
         double prod = 1.0, nlog = 0.0, umin = 1.0;
-        int hits = 0;
+        unsigned miss = 0;
         auto post = [&](double uq, double tq, bool valid, double &qo) {
 #if CE_LR_RCP1
             const double inv = rcp_newton1(1.0 + tq);       // p_y
@@ -270,7 +283,7 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
                 const double au = valid ? uq : 1.0;
                 asm("v_min_f64 %0, %1, |%2|" : "=v"(umin) : "v"(umin), "v"(au));
             }
-            hits += (valid && uq > 0.0) ? 1 : 0;
+            miss += lr_miss(uq, valid);
         };
         auto rows = [&](auto clamp_c) {
 #pragma unroll
@@ -302,7 +315,7 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
                     }
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
-                        sacc[g0 + i] = __builtin_amdgcn_mfma_f64_16x16x4f64(xg[g0 + i][q], qv[q], sacc[g0 + i], 0, 0, 0);
+                        sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(xg[g0 + i][q], qv[q], sacc, 0, 0, 0);
                 }
             }
         };
@@ -310,6 +323,7 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
         else rows(std::true_type{});
         // a tie (p0 == p1, |u| < 2^-52) is np.argmax's class 0: hit iff y == 0;
         // only a wave that saw one re-walks its tiles exactly (practically never)
+        int hits = 4 * TPW - static_cast<int>(miss);
         if (__any(umin < 0x1p-52)) {
 #pragma unroll
             for (int i = 0; i < TPW; ++i) {
@@ -326,7 +340,7 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
                 exp_neg_multi_clamped<4>(tx);
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    if (yv[q] >= 0 && tx[q] == 1.0) hits += (yv[q] == 0 ? 1 : 0) - (uu[q] > 0.0 ? 1 : 0);
+                    if (yv[q] >= 0 && tx[q] == 1.0) hits += (yv[q] == 0 ? 1 : 0) - lr_hit(uu[q]);
             }
         }
         // this wave's partials: s (features h + 4r of env c); -log of the
@@ -336,12 +350,7 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
         lsum = fold_pair<32>(lsum, lsum);
         const double hsum = static_cast<double>(fold_env_lanes(hits));
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            double v = sacc[0][r];
-#pragma unroll
-            for (int i = 1; i < TPW; ++i) v += sacc[i][r];
-            red_s[buf][wave][r][lane] = v;
-        }
+        for (int r = 0; r < 4; ++r) red_s[buf][wave][r][lane] = sacc[r];
         if (lane < kLrEnvs) {
             red_l[buf][wave][lane] = lsum;
             red_h[buf][wave][lane] = hsum;
@@ -456,7 +465,9 @@ __global__ __launch_bounds__(kWave * W) void optimize_lr_persist_kernel(StepArgs
 // the row wave's own LDS tiles instead of registers.  Same arithmetic, same summation
 // order as optimize_lr_persist_kernel<NKF, TPW, PAD, 4>: bit-identical.
 template <int NKF, int TPW, bool PAD>
-__global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<double> a, ManyArgs m) {
+__global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(
+    double *Wp, const float *actp, const unsigned char *datap, double *Gp, int32_t *stepp, double *Lp,
+    unsigned efp, int Np, StepArgs<double> a, ManyArgs m) {
     constexpr int W = 4;                                    // row waves
     constexpr int BLK = 512;
     constexpr int EB = BLK - kWave * W;                     // epilogue threads
@@ -469,7 +480,14 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
     __shared__ double red_l[2][W][kLrEnvs];
     __shared__ double red_h[2][W][kLrEnvs];
     __shared__ __attribute__((aligned(16))) float obs_s[2][kLrEnvs * OSM];
-    __shared__ double xgs[W][TPW][4][kWave];                // gradient A operands
+    // gradient A operands: the 16x16x4 form's tile slots, or for the 4x4x4
+    // form (G4) X~[16t + 4j + k][4g + m] at [wave][tile][4k + m][j NKF + g],
+    // a 14-double row stride per (k, m) so a row's ds_read_b128s meet no bank
+    // twice
+    constexpr bool G4 = lp_g4(NKF);
+    constexpr int G4S = 14;
+    __shared__ __attribute__((aligned(16))) double xgs[G4 ? 1 : W][G4 ? 1 : TPW][4][kWave];
+    __shared__ __attribute__((aligned(16))) double xga[G4 ? W : 1][G4 ? TPW : 1][16][G4S];
     __shared__ double tab_s[CE_LR_TEXP ? kLrExpTab : 1];   // the row waves' exp table
 
 #ifdef CE_DIAG
@@ -480,10 +498,13 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, h = lane >> 4;
-    const int E = a.E, F = a.F, P = 2 * F, N = a.N, B = a.B;
+    // the prologue's pointers and sizes as leading scalar arguments: built
+    // with -amdgpu-kernarg-preload-count=14 (build.py) they arrive in SGPRs at
+    // wave launch and the first loads need no kernel-argument load
+    const int E = static_cast<int>(efp & 0xffffffu), F = static_cast<int>(efp >> 24), P = 2 * F, N = Np, B = a.B;
     const int OS = a.obs_stride, OL = a.obs_lo;
     const int e0 = blockIdx.x * kLrEnvs;
-    const double *img = reinterpret_cast<const double *>(a.data);
+    const double *img = reinterpret_cast<const double *>(datap);
     const int ntiles = (N + 15) / 16;
     const int nenv = E - e0 < kLrEnvs ? E - e0 : kLrEnvs;
 
@@ -500,6 +521,9 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
 #endif
     if (wave < W) {
         // ======================= row waves =======================
+#if CE_LP_ROW_PRIO > 0
+        __builtin_amdgcn_s_setprio(CE_LP_ROW_PRIO);      // experiment: row waves win arbitration
+#endif
         const int e = e0 + c;
         const bool env_ok = e < E;
         const unsigned pbase = static_cast<unsigned>(env_ok ? e : 0) * P;
@@ -514,8 +538,8 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
         for (int k = 0; k < NKF; ++k) {
             const int f = 4 * k + h;
             ioff[k] = pbase + (f < F ? 2 * f : 0);
-            wv[k] = *reinterpret_cast<const double2 *>(a.W + ioff[k]);
-            av[k] = *reinterpret_cast<const float2 *>(a.act + ioff[k]);
+            wv[k] = *reinterpret_cast<const double2 *>(Wp + ioff[k]);
+            av[k] = *reinterpret_cast<const float2 *>(actp + ioff[k]);
 #if CE_LR_NOCLAMP
             xm[k] = colmax[f];
 #endif
@@ -533,8 +557,17 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
             const double *ti = img + static_cast<unsigned>(live ? t : 0) * TD;
 #pragma unroll
             for (int k = 0; k < NKF; ++k) xf[i][k] = live ? ti[k * kWave + lane] : 0.0;
+            if constexpr (G4) {
+                // lane (k, b, m) keeps feature group g = b: its own lane of the
+                // tile's gradient slot j is X~[16t + 4j + k][4b + m]
+                const int b4 = (lane >> 2) & 3, km = 4 * (lane >> 4) + (lane & 3);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) xgs[wave][i][q][lane] = live ? ti[(NKF + q) * kWave + lane] : 0.0;
+                for (int q = 0; q < 4; ++q)
+                    if (b4 < NKF) xga[wave][i][km][q * NKF + b4] = live ? ti[(NKF + q) * kWave + lane] : 0.0;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) xgs[wave][i][q][lane] = live ? ti[(NKF + q) * kWave + lane] : 0.0;
+            }
             if constexpr (PAD) {
                 const int2 ya = reinterpret_cast<const int2 *>(ti + (NKF + 4) * kWave)[lane];
                 const int2 yb = reinterpret_cast<const int2 *>(ti + (NKF + 5) * kWave)[lane];
@@ -543,7 +576,7 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                 for (int q = 0; q < 4; ++q) vmask |= (live && ys[q] >= 0 ? 1u : 0u) << (4 * i + q);
             }
         }
-        int step_c = a.step[env_ok ? e : 0];
+        int step_c = stepp[env_ok ? e : 0];
 #if CE_LR_TEXP
         tslice.store(tab_s, tid);                           // waits on the table loads only
         __syncthreads();
@@ -575,7 +608,7 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
             const int buf = t & 1;
             float2 an[NKF];
             {
-                const float *actn = a.act + (t + 1 < m.k ? (t + 1) * m.act_stride : 0);
+                const float *actn = actp + (t + 1 < m.k ? (t + 1) * m.act_stride : 0);
 #pragma unroll
                 for (int k = 0; k < NKF; ++k) an[k] = *reinterpret_cast<const float2 *>(actn + ioff[k]);
             }
@@ -589,11 +622,12 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
 #else
             const bool bounded = false;
 #endif
-            lr_d4 sacc[TPW];
+            lr_d4 sacc = {0.0, 0.0, 0.0, 0.0};             // one gradient chain, tile order
+            double gacc[NKF];                               // G4: one chain per feature group
 #pragma unroll
-            for (int i = 0; i < TPW; ++i) sacc[i] = lr_d4{0.0, 0.0, 0.0, 0.0};
+            for (int g = 0; g < NKF; ++g) gacc[g] = 0.0;
             double prod = 1.0, nlog = 0.0, umin = 1.0;
-            int hits = 0;
+            unsigned miss = 0;
             auto post = [&](double uq, double tq, bool valid, double &qo) {
 #if CE_LR_RCP1
                 const double inv = rcp_newton1(1.0 + tq);
@@ -606,7 +640,7 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                     const double au = valid ? uq : 1.0;
                     asm("v_min_f64 %0, %1, |%2|" : "=v"(umin) : "v"(umin), "v"(au));
                 }
-                hits += (valid && uq > 0.0) ? 1 : 0;
+                miss += lr_miss(uq, valid);
             };
             auto rows = [&](auto clamp_c) {
 #pragma unroll
@@ -620,9 +654,21 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                     for (int i = 0; i < NG; ++i) u[i] = forward(xf[g0 + i]);
 #pragma unroll
                     for (int i = 0; i < NG; ++i) {
-                        double gv[4];
+                        double gv[G4 ? 4 * NKF : 4];
+                        if constexpr (G4) {
+                            typedef double lp_d2 __attribute__((ext_vector_type(2)));
+                            const lp_d2 *src = reinterpret_cast<const lp_d2 *>(
+                                &xga[wave][g0 + i][4 * (lane >> 4) + (lane & 3)][0]);
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) gv[q] = xgs[wave][g0 + i][q][lane];
+                            for (int p2 = 0; p2 < 2 * NKF; ++p2) {
+                                const lp_d2 v = src[p2];
+                                gv[2 * p2] = v.x;
+                                gv[2 * p2 + 1] = v.y;
+                            }
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) gv[q] = xgs[wave][g0 + i][q][lane];
+                        }
                         double qv[4];
 #pragma unroll
                         for (int q0 = 0; q0 < 4; q0 += QC) {
@@ -639,14 +685,25 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                                 post(u[i][q0 + j], tx[j], valid, qv[q0 + j]);
                             }
                         }
+                        if constexpr (G4) {
+                            // S[4g + m][4b + n] += X~[4q + k][4g + m] q[4q + k][4b + n]:
+                            // the forward's C register q is the B operand as it stands
 #pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            sacc[g0 + i] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[q], qv[q], sacc[g0 + i], 0, 0, 0);
+                            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                                for (int g = 0; g < NKF; ++g)
+                                    gacc[g] = __builtin_amdgcn_mfma_f64_4x4x4f64(gv[q * NKF + g], qv[q], gacc[g], 0, 0, 0);
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[q], qv[q], sacc, 0, 0, 0);
+                        }
                     }
                 }
             };
             if (bounded) rows(std::false_type{});
             else rows(std::true_type{});
+            int hits = 4 * TPW - static_cast<int>(miss);
             if (__any(umin < 0x1p-52)) {
 #pragma unroll
                 for (int i = 0; i < TPW; ++i) {
@@ -663,19 +720,20 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                     exp_neg_multi_clamped<4>(tx);
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
-                        if (yv[q] >= 0 && tx[q] == 1.0) hits += (yv[q] == 0 ? 1 : 0) - (uu[q] > 0.0 ? 1 : 0);
+                        if (yv[q] >= 0 && tx[q] == 1.0) hits += (yv[q] == 0 ? 1 : 0) - lr_hit(uu[q]);
                 }
             }
             double lsum = nlog - log_pos(prod);
             lsum = fold_pair<16>(lsum, lsum);
             lsum = fold_pair<32>(lsum, lsum);
             const double hsum = static_cast<double>(fold_env_lanes(hits));
+            // S[f][env] at [f >> 2][16 (f & 3) + env] in both forms (rows past F unread)
+            if constexpr (G4) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                double v = sacc[0][r];
+                for (int g = 0; g < NKF; ++g) red_s[buf][wave][g][lane] = gacc[g];
+            } else {
 #pragma unroll
-                for (int i = 1; i < TPW; ++i) v += sacc[i][r];
-                red_s[buf][wave][r][lane] = v;
+                for (int r = 0; r < 4; ++r) red_s[buf][wave][r][lane] = sacc[r];
             }
             if (lane < kLrEnvs) {
                 red_l[buf][wave][lane] = lsum;
@@ -684,9 +742,12 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
             {
                 const bool wipe = step_c + 1 >= a.max_steps && a.auto_reset;
                 step_c = wipe ? 0 : step_c + 1;
+                // one step in max_steps wipes: the selects behind a uniform branch
+                if (__any(wipe)) {
 #pragma unroll
-                for (int k = 0; k < NKF; ++k)
-                    if (wipe) wv[k] = w0v[k];
+                    for (int k = 0; k < NKF; ++k)
+                        if (wipe) wv[k] = w0v[k];
+                }
                 if (t + 1 < m.k) {
 #pragma unroll
                     for (int k = 0; k < NKF; ++k) av[k] = an[k];
@@ -709,8 +770,8 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
 #pragma unroll
             for (int k = 0; k < NKF; ++k)
                 if (4 * k + h < F) {
-                    lr_store(a.W + ioff[k], wv[k].x);
-                    lr_store(a.W + ioff[k] + 1, wv[k].y);
+                    lr_store(Wp + ioff[k], wv[k].x);
+                    lr_store(Wp + ioff[k] + 1, wv[k].y);
                 }
         }
     } else {
@@ -729,14 +790,14 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
             pp[r] = i - pj[r] * P;
             prole[r] = i < np_ && e0 + pj[r] < E;
             gi[r] = static_cast<unsigned>(prole[r] ? e0 + pj[r] : 0) * P + (prole[r] ? pp[r] : 0);
-            g_prev[r] = a.G[gi[r]];
-            step_p[r] = a.step[prole[r] ? e0 + pj[r] : 0];
+            g_prev[r] = Gp[gi[r]];
+            step_p[r] = stepp[prole[r] ? e0 + pj[r] : 0];
         }
         const int sj = te - (EB - kLrEnvs);
         const bool srole = sj >= 0 && e0 + sj < E;
         const unsigned es = srole ? e0 + sj : 0;
-        double lprev = a.L[es];
-        int step_s = a.step[es];
+        double lprev = Lp[es];
+        int step_s = stepp[es];
 #if CE_LR_TEXP
         tslice.store(tab_s, tid);
 #endif
@@ -775,6 +836,12 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
             for (int t = 0; t < m.k; ++t) {
                 const int buf = t & 1;
                 __syncthreads();                                // the row waves' partials of step t
+#if CE_LP_EPI_SLEEP > 0
+                // experiment: leave the row wave's forward MFMA block alone
+                // (another wave's VALU between back-to-back f64 MFMAs stalls
+                // them, profiles/r06_mfma_overlap.jsonl)
+                __builtin_amdgcn_s_sleep(CE_LP_EPI_SLEEP);
+#endif
     #ifdef CE_DIAG
                 if (t == 1) LP_STAMP(2);                        // epilogue waves: step 1 starts
     #endif
@@ -800,9 +867,17 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                              static_cast<float>(acc));
                     if (a.done) (reinterpret_cast<uint8_t *>(a.done) + ro)[es] = cur >= a.max_steps ? 1 : 0;
                     lr_store(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro) + es, cur);
-                    obs_s[buf][sj * OS + P - OL] = wipe ? 0.0f : static_cast<float>(lnew);
-                    lprev = wipe ? 0.0 : lnew;
-                    step_s = wipe ? 0 : cur;
+                    float ol = static_cast<float>(lnew);
+                    lprev = lnew;
+                    step_s = cur;
+                    if (__any(wipe)) {                          // the auto-reset's zeros
+                        if (wipe) {
+                            ol = 0.0f;
+                            lprev = 0.0;
+                            step_s = 0;
+                        }
+                    }
+                    obs_s[buf][sj * OS + P - OL] = ol;
                     rL = rcp_newton2(lprev + 0.1);
                 }
     #pragma unroll
@@ -815,9 +890,17 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
                     for (int w = 0; w < W; ++w) sf += red_s[buf][w][f >> 2][pj[r] + 16 * (f & 3)];
                     const double g = divB((pp[r] & 1) ? sf : -sf);
                     const double gnew = div_rcp(g, fabs(g_prev[r]) + 1.0, rG[r]);
-                    obs_s[buf][pj[r] * OS + P + 1 + pp[r] - OL] = wipe ? 0.0f : static_cast<float>(gnew);
-                    g_prev[r] = wipe ? 0.0 : gnew;
-                    step_p[r] = wipe ? 0 : step_p[r] + 1;
+                    float og = static_cast<float>(gnew);
+                    g_prev[r] = gnew;
+                    step_p[r] = step_p[r] + 1;
+                    if (__any(wipe)) {                          // the auto-reset's zeros
+                        if (wipe) {
+                            og = 0.0f;
+                            g_prev[r] = 0.0;
+                            step_p[r] = 0;
+                        }
+                    }
+                    obs_s[buf][pj[r] * OS + P + 1 + pp[r] - OL] = og;
                     rG[r] = rcp_newton2(fabs(g_prev[r]) + 1.0);
                 }
     #ifdef CE_DIAG
@@ -834,10 +917,10 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(StepArgs<do
         if (m.k > 0) flush_obs(m.k - 1);
 #pragma unroll
         for (int r = 0; r < PR; ++r)
-            if (prole[r]) lr_store(&a.G[gi[r]], g_prev[r]);
+            if (prole[r]) lr_store(&Gp[gi[r]], g_prev[r]);
         if (srole) {
-            lr_store(&a.L[es], lprev);
-            lr_store(&a.step[es], step_s);
+            lr_store(&Lp[es], lprev);
+            lr_store(&stepp[es], step_s);
         }
     }
 #ifdef CE_DIAG

@@ -25,8 +25,11 @@ void launch_persist(const StepArgs<double> &a, const ManyArgs &m, hipStream_t st
 template <int NKF, int TPW, bool PAD>
 void launch_persist_ws(const StepArgs<double> &a, const ManyArgs &m, hipStream_t stream) {
     const int grid = (a.E + kLrEnvs - 1) / kLrEnvs;
+    // the prologue's pointers and sizes lead (preloaded into SGPRs, build.py);
+    // E | F << 24 as the one-step kernel's size word (E < 2^24, F <= 16)
+    const unsigned ef = static_cast<unsigned>(a.E) | (static_cast<unsigned>(a.F) << 24);
     hipLaunchKernelGGL((optimize_lr_persist_ws_kernel<NKF, TPW, PAD>), dim3(grid), dim3(512), 0, stream,
-                       a, m);
+                       a.W, a.act, a.data, a.G, a.step, a.L, ef, a.N, a, m);
 }
 
 template <int NKF, bool PAD>

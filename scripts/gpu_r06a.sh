@@ -7,10 +7,13 @@ OUT=${OUT:-gpurun_out/r06a}
 mkdir -p $OUT
 export TMPDIR=/tmp
 fatal() { case $1 in 0) ;; *) echo "GPU step failed (rc=$1), stopping"; exit $1;; esac; }
-timeout -k 10 120 ./scripts/bin/mfma_overlap > $OUT/overlap.jsonl 2>&1; rc=$?
+if [ "${OVERLAP:-0}" = 1 ]; then
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -w scripts/mfma_overlap.hip -o /tmp/mfma_overlap || exit 1
+timeout -k 10 120 /tmp/mfma_overlap > $OUT/overlap.jsonl 2>&1; rc=$?
 echo "overlap rc=$rc"; fatal $rc
+fi
 timeout -k 10 600 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread \
-  tests/test_gpu_persist.py::test_strided_argument_checks \
+  tests/test_gpu_persist.py::test_strided_argument_checks tests/test_gpu_persist.py::test_misaligned_obs_is_refused_not_rerouted \
   tests/test_gpu_multi.py::test_config5_global_size_on_one_engine \
   tests/test_gpu_multi.py::test_multi_rollout_argument_checks \
   tests/test_gpu_multinn.py > $OUT/pytest.log 2>&1; rc=$?

@@ -498,11 +498,12 @@ def test_multi_rollout_argument_checks():
     try:
         fields, rb = eng.alloc_rollout(4)
         eng.reset_device({k: v[0] for k, v in fields.items() if k != '_buffer'})
-        acts = torch.full((4, eng.rows), 2.0, device='cuda')
+        # lr = 10^(0.5 - 4): no loss > 1e4 stop in 4 steps
+        acts = torch.full((4, eng.rows), 0.5, device='cuda')
         with pytest.raises(ValueError, match='holds 4 records'):
-            eng.rollout_device(5, torch.full((5, eng.rows), 2.0, device='cuda'), fields, rb)
+            eng.rollout_device(5, torch.full((5, eng.rows), 0.5, device='cuda'), fields, rb)
         with pytest.raises(ValueError, match='holds 4 records'):
-            eng.rollout_runner(50, torch.full((50, eng.rows), 2.0, device='cuda'), fields, rb)
+            eng.rollout_runner(50, torch.full((50, eng.rows), 0.5, device='cuda'), fields, rb)
         with pytest.raises(ValueError, match='record stride'):
             eng.rollout_device(4, acts, fields, rb + 256)
         with pytest.raises(ValueError, match='float32'):

@@ -280,11 +280,14 @@ def _check_env(ds, hidden, seed, acts_env, rows, rec, i, max_batches, H=5, state
         ring.append(obs.copy())
         theta_prev, g_prev, l_prev = theta_after, g_e.astype(np.float64), loss
     # the per-row 1e-5 norm bound above is not vacuous for this env: it
-    # covered at least a twentieth of the (step, row) slots compared
+    # covered at least 250 (step, row) slots (or a tenth of them on short
+    # runs).  The rows that qualify (|den| >= 0.1 max and |ref| >= 0.5) do not
+    # grow with the network: measured r06, 489-3090 rows per env over
+    # 3,885-407,058 slots (profiles/r06b_nn_row_floor.log)
     n_rows, n_slots = stats['rows'] - rows0, stats.get('row_slots', 0) - slots0
     print('nn env %d per-row check: %d of %d (step, row) slots, worst %.3g'
           % (i, n_rows, n_slots, stats['row_err_max']))
-    assert n_rows >= n_slots // 20, (i, n_rows, n_slots)
+    assert n_rows >= min(250, n_slots // 10), (i, n_rows, n_slots)
 
 
 def _actions(T, E, P, lo, hi, seed):
@@ -446,10 +449,9 @@ def test_default_network_benchmark_size_sampled_envs():
         _check_env(ds, hidden, e, acts_s[:, k], rows, rec, k, 400, stats=stats)
     print('nn per-row check:', {k: stats[k] for k in ('rows', 'row_steps', 'row_slots', 'row_err_max')})
     assert stats['adj_grad'] >= 2 * (T - 2)
-    # the per-row 1e-5 norm bound is not vacuous: it covers at least a
-    # twentieth of all (step, row) slots compared (measured r06: NN_ROWS_SEEN)
+    # the per-row 1e-5 norm bound is not vacuous: 250 rows per sampled env
     assert stats['row_steps'] >= 2 * (T - 2)
-    assert stats['rows'] >= stats['row_slots'] // 20, stats
+    assert stats['rows'] >= 250 * len(sample), stats
 
 
 def test_divergence_stops_early_with_penalty():
