@@ -292,3 +292,56 @@ def test_misaligned_obs_is_refused_not_rerouted(lr_dataset):
     eng.wait()
     assert int(bad['episode_len'][0]) == 3
     eng.close()
+
+
+@pytest.mark.parametrize('paired', [True, False])
+def test_set_state_grad_hist_then_k_steps(lr_dataset, paired):
+    """From a ce_set_state grad_hist -- exactly negated column pairs (what the
+    kernels themselves write: column 1 of X^T (P - Y) is column 0 negated) or
+    unpaired in some workgroups -- every output of every step and the final
+    state of persistent launches equal per-step launches (r06: a feature-pair
+    epilogue that relied on the pairing measured no gain and was withdrawn)."""
+    E, P, T = 100, 20, 45                      # 7 workgroups, a partial last one
+    rs = np.random.RandomState(21 if paired else 22)
+    acts = rs.normal(0, 0.01, (T, E, P)).astype(np.float32)
+    g = rs.normal(0, 0.5, (E, P // 2))
+    grad = np.empty((E, P))
+    grad[:, 0::2] = g
+    grad[:, 1::2] = -g
+    if not paired:
+        grad[::3, 1::2] += rs.normal(0, 0.1, (len(range(0, E, 3)), P // 2))   # some workgroups unpaired
+    outs = []
+    for persist in (False, True):
+        eng = _engine(lr_dataset, E, persistent=persist)
+        eng.seed(list(range(E)))
+        eng.reset()
+        st = eng.get_state()
+        st['grad_hist'] = grad
+        eng.set_state(**{k: v for k, v in st.items() if k != 'order'})
+        got, st_end = _rollout_from_state(eng, acts, [20, 20, 5])
+        outs.append((got, st_end))
+        eng.close()
+    (a, sa), (b, sb) = outs
+    for name in FIELDS:
+        assert np.array_equal(a[name], b[name]), name
+    for name in ('weights', 'grad_hist', 'loss_hist', 'step'):
+        assert np.array_equal(sa[name], sb[name]), name
+
+
+def _rollout_from_state(eng, acts, chunks):
+    """As _rollout, but from the engine's current state (no seed / reset)."""
+    import torch
+    stream = torch.cuda.Stream()
+    rec = {k: [] for k in FIELDS}
+    with torch.cuda.stream(stream):
+        eng.set_stream(stream.cuda_stream)
+        dact = torch.from_numpy(acts).cuda()
+        t = 0
+        for k in chunks:
+            fields, rb = eng.alloc_rollout(k)
+            eng.rollout_device(k, dact[t:t + k], fields, rb)
+            stream.synchronize()
+            for name in FIELDS:
+                rec[name].append(fields[name].cpu().numpy())
+            t += k
+    return {k: np.concatenate(v) for k, v in rec.items()}, eng.get_state()
