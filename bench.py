@@ -1050,7 +1050,8 @@ def _common(args, world, E, S, elapsed, shard):
 # (scripts/traffic.py).  The committed summaries of this round are named here
 # and reported in roofline.traffic_source; --measure-traffic takes them in
 # the run instead.
-TRAFFIC_ROUND = 'r05'
+TRAFFIC_ROUND = 'r06'
+TRAFFIC_FALLBACK_ROUNDS = ('r06', 'r05')     # committed summaries, newest first
 TRAFFIC_MARKER = {'optimize': 'optimize_lr_', 'multi': 'multi_',
                   'mlp': 'mlp_step_kernel', 'net': 'net_finish_kernel',
                   'nn': 'nn_finalize_kernel', 'mnist': 'optimize_'}
@@ -1098,7 +1099,10 @@ def traffic_fields(args, eng, E, bpe=None):
             why = 'in-run measurement failed (%s); ' % str(exc)[:160]
     else:
         why = ''
-    path = os.path.join(ROOT, 'profiles', '%s_traffic_%s.json' % (TRAFFIC_ROUND, name))
+    for rnd in TRAFFIC_FALLBACK_ROUNDS:
+        path = os.path.join(ROOT, 'profiles', '%s_traffic_%s.json' % (rnd, name))
+        if os.path.exists(path):
+            break
     if not os.path.exists(path):
         return {'traffic': None, 'traffic_source': why + 'no %s' % os.path.relpath(path, ROOT)}
     with open(path) as fh:

@@ -85,6 +85,13 @@ typedef double lr_d4 __attribute__((ext_vector_type(4)));
 #ifndef CE_LR_TEXP
 #define CE_LR_TEXP 1
 #endif
+//  CE_LR_TGLOBAL  the one-step kernel reads the table entries straight from
+//                 the image in global memory (L1 / L2) instead of copying the
+//                 16 KB into LDS behind a barrier first (the K-step kernels
+//                 keep their LDS copy: they pay for it once per K steps)
+#ifndef CE_LR_TGLOBAL
+#define CE_LR_TGLOBAL 0
+#endif
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)
 
@@ -257,7 +264,8 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     // the exp table, one copy per workgroup (one per wave at 4 waves, with no
     // barrier before the first lookup, measured 6.5e8 -> 5.9-6.1e8 env-steps/s
     // per-step launch, profiles/r05ai_*)
-    __shared__ double tab_s[CE_LR_TEXP ? kLrExpTab : 1];
+    constexpr bool TLDS = CE_LR_TEXP && !CE_LR_TGLOBAL;  // the table copied into LDS
+    __shared__ double tab_s[TLDS ? kLrExpTab : 1];
 #ifdef CE_DIAG
     unsigned long long stamps[kStamps] = {0};
     stamps[6] = __builtin_amdgcn_s_memrealtime();
@@ -288,10 +296,12 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     //    G and W0 of parameter p of env e0 + j and that env's step counter;
     //  - role "scalar" (the last 16 threads, one per env of the group): L
     //    and the step counter.
-#if CE_LR_TEXP
-    // the exp table behind the image's column maxima, the first loads issued
+    // the exp table behind the image's column maxima
+    const double *tab_g = img + static_cast<unsigned>(ntiles) * TD + kLrMaxF;
+#if CE_LR_TEXP && !CE_LR_TGLOBAL
+    // its LDS copy: the first loads issued
     LrExpSlice<kLrBlock> tslice;
-    tslice.load(img + static_cast<unsigned>(ntiles) * TD + kLrMaxF, tid);
+    tslice.load(tab_g, tid);
 #endif
     double2 wv[NKF];
     float2 av[NKF];
@@ -360,7 +370,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     const unsigned es = srole ? e0 + sj : 0;
     const double lprev = Lp[es];
     const int step_prev = stepp[es];
-#if CE_LR_TEXP
+#if CE_LR_TEXP && !CE_LR_TGLOBAL
     tslice.store(tab_s, tid);                           // waits on the table loads only
 #endif
 
@@ -426,7 +436,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
     for (int r = 0; r < PR; ++r)
         if (prole[r] && step_p[r] + 1 >= a.max_steps && a.auto_reset) w_init[r] = a.W0[gi[r]];
 #endif
-#if CE_LR_TEXP
+#if CE_LR_TEXP && !CE_LR_TGLOBAL
     __syncthreads();                                    // the table, before the first lookup
 #endif
 #ifdef CE_DIAG
@@ -478,7 +488,7 @@ __global__ __launch_bounds__(LrShape<W>::kBlock) void optimize_lr_mfma_kernel(
                 if constexpr (decltype(clamp_c)::value) tx[i] = clamp_u(u[q0 + i]);
                 else tx[i] = u[q0 + i];
             }
-            lr_exp_neg<QC>(tx, tab_s);                  // t = e^-u
+            lr_exp_neg<QC>(tx, TLDS ? tab_s : tab_g);   // t = e^-u
 #pragma unroll
             for (int i = 0; i < QC; ++i) post(u[q0 + i], tx[i], ys[q0 + i], qv[q0 + i]);
         }
