@@ -23,6 +23,12 @@ if [ "${PROBE:-0}" = 1 ]; then
   timeout -k 10 60 /tmp/mfma4x4_layout > $OUT/mfma4x4_layout.json 2>&1; rc=$?
   echo "probe rc=$rc"; fatal $rc
 fi
+if [ "${DIAG:-0}" = 1 ]; then
+  # phase stamps of the K-step kernel (CE_LIB=diag builds the stamp library
+  # on the box from the pushed sources: it never travels)
+  CE_LIB=diag timeout -k 10 600 python -u scripts/diag_persist.py --k 20 250 > $OUT/diag_persist.jsonl 2> $OUT/diag.err; rc=$?
+  echo "diag rc=$rc"; cat $OUT/diag_persist.jsonl | cut -c1-600; fatal $rc
+fi
 for rep in $(seq 1 ${REPS:-2}); do
   for lib in ${LIBS:-default prev}; do
     if [ $lib = default ]; then L=""; else L=$lib; fi
