@@ -90,7 +90,7 @@ typedef double lr_d4 __attribute__((ext_vector_type(4)));
 //                 16 KB into LDS behind a barrier first (the K-step kernels
 //                 keep their LDS copy: they pay for it once per K steps)
 #ifndef CE_LR_TGLOBAL
-#define CE_LR_TGLOBAL 0
+#define CE_LR_TGLOBAL 1
 #endif
 
 constexpr int kLrEnvs = 16;                    // envs per workgroup (MFMA N)

@@ -51,6 +51,11 @@ constexpr int kLpMaxTpw = 8;                  // row tiles a wave keeps in regis
 #ifndef CE_LP_G4
 #define CE_LP_G4 1
 #endif
+// the 4x4x4 gradient's A operands transposed in-kernel from the forward
+// operands (CE_LP_G4_XF=1) or loaded from the image's gradient slots (0)
+#ifndef CE_LP_G4_XF
+#define CE_LP_G4_XF 1
+#endif
 #ifndef CE_LP_EPI_SLEEP
 #define CE_LP_EPI_SLEEP 0
 #endif
@@ -558,12 +563,22 @@ __global__ __launch_bounds__(512) void optimize_lr_persist_ws_kernel(
 #pragma unroll
             for (int k = 0; k < NKF; ++k) xf[i][k] = live ? ti[k * kWave + lane] : 0.0;
             if constexpr (G4) {
+#if CE_LP_G4_XF
+                // from the forward operands already in registers (no second
+                // copy of the tile read from L2 in the prologue): lane (h, c)
+                // holds X~[16t + c][4g + h] = xf[i][g], the A value of slot
+                // (k = c & 3, m = h), column j = c >> 2, group g
+                const int km = 4 * (c & 3) + h, j4 = c >> 2;
+#pragma unroll
+                for (int g = 0; g < NKF; ++g) xga[wave][i][km][j4 * NKF + g] = xf[i][g];
+#else
                 // lane (k, b, m) keeps feature group g = b: its own lane of the
                 // tile's gradient slot j is X~[16t + 4j + k][4b + m]
                 const int b4 = (lane >> 2) & 3, km = 4 * (lane >> 4) + (lane & 3);
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     if (b4 < NKF) xga[wave][i][km][q * NKF + b4] = live ? ti[(NKF + q) * kWave + lane] : 0.0;
+#endif
             } else {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) xgs[wave][i][q][lane] = live ? ti[(NKF + q) * kWave + lane] : 0.0;

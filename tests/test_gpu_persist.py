@@ -181,6 +181,8 @@ def test_1000_steps_every_slot_against_oracle(lr_dataset):
     (40, 10, 'optimize_lr_persist_ws_kernel<3,1,true>'),
     (100, 4, 'optimize_lr_persist_ws_kernel<1,2,true>'),
     (128, 16, 'optimize_lr_persist_ws_kernel<4,2,false>'),
+    (192, 6, 'optimize_lr_persist_ws_kernel<2,4,true>'),
+    (256, 8, 'optimize_lr_persist_ws_kernel<2,4,false>'),
     (512, 7, 'optimize_lr_persist_kernel<2,8,false,4>'),
     (300, 13, 'optimize_lr_persist_kernel<4,8,true,4>'),
 ])
@@ -345,3 +347,24 @@ def _rollout_from_state(eng, acts, chunks):
                 rec[name].append(fields[name].cpu().numpy())
             t += k
     return {k: np.concatenate(v) for k, v in rec.items()}, eng.get_state()
+
+
+@pytest.mark.parametrize('n_rows,n_features', [(100, 4), (192, 6), (256, 8), (40, 10), (128, 16)])
+def test_forms_bit_equal_to_one_step_launches(n_rows, n_features):
+    """The K-step kernel's gradient on 4x4x4 f64 blocks (feature groups
+    NKF = 1, 2, 3; 16x16x4 at NKF = 4), padded and unpadded row tiles: every
+    output of every step and the state equal one-step launches (which keep
+    the 16x16x4 gradient) bit for bit."""
+    data = _dataset(n_rows, n_features, 7 * n_rows + n_features)
+    E, P, T = 37, 2 * n_features, 45
+    acts = np.random.RandomState(n_features).normal(0, 0.01, (T, E, P)).astype(np.float32)
+    outs = []
+    for persist in (False, True):
+        eng = _engine(data, E, persistent=persist)
+        outs.append(_rollout(eng, range(E), acts, [20, 20, 5]))
+        eng.close()
+    (a, sa), (b, sb) = outs
+    for name in FIELDS:
+        assert np.array_equal(a[name], b[name]), name
+    for name in ('weights', 'grad_hist', 'loss_hist', 'step'):
+        assert np.array_equal(sa[name], sb[name]), name
