@@ -350,17 +350,22 @@ def _rollout_from_state(eng, acts, chunks):
 
 
 @pytest.mark.parametrize('n_rows,n_features', [(100, 4), (192, 6), (256, 8), (40, 10), (128, 16)])
-def test_forms_bit_equal_to_one_step_launches(n_rows, n_features):
+def test_forms_bit_equal_to_one_step_launches(n_rows, n_features, monkeypatch):
     """The K-step kernel's gradient on 4x4x4 f64 blocks (feature groups
     NKF = 1, 2, 3; 16x16x4 at NKF = 4), padded and unpadded row tiles: every
     output of every step and the state equal one-step launches (which keep
-    the 16x16x4 gradient) bit for bit."""
+    the 16x16x4 gradient) bit for bit.  The one-step kernel is held to its
+    4-wave form (CE_LR_WAVES=4), the K-step kernel's tile -> wave split: at
+    this E it would pick 8 waves, whose partials meet in another order."""
     data = _dataset(n_rows, n_features, 7 * n_rows + n_features)
     E, P, T = 37, 2 * n_features, 45
     acts = np.random.RandomState(n_features).normal(0, 0.01, (T, E, P)).astype(np.float32)
+    monkeypatch.setenv('CE_LR_WAVES', '4')
     outs = []
     for persist in (False, True):
         eng = _engine(data, E, persistent=persist)
+        if not persist:
+            assert eng.step_kernel.endswith(',4>'), eng.step_kernel
         outs.append(_rollout(eng, range(E), acts, [20, 20, 5]))
         eng.close()
     (a, sa), (b, sb) = outs
