@@ -52,6 +52,10 @@ else
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$name -o run --output-format csv -- python3 bench.py $pargs --profile-only --steps 10 --warmup 2 > $OUT/prof_$name.log 2>&1; rc=$?
     echo "rocprof $name rc=$rc"; fatal $rc
   done
+  # config 4's global batch on one GPU: the open-loop value and the
+  # closed-loop (one launch per step) rate at 32,768 envs
+  timeout -k 10 300 python bench.py --envs 32768 --steps 2000 --warmup 200 --no-cpu-baseline --no-measure-traffic > $OUT/bench_e32768.log 2>&1; rc=$?
+  echo "bench e32768 rc=$rc"; summ $OUT/bench_e32768.log e32768; fatal $rc
   timeout -k 10 300 python bench.py --force-gather --no-cpu-baseline --steps 2000 --warmup 200 > $OUT/bench_gather.log 2>&1; rc=$?
   echo "bench gather rc=$rc"; summ $OUT/bench_gather.log gather; fatal $rc
   timeout -k 10 300 python bench.py --force-gather --no-cpu-baseline --steps 20 --warmup 5 > $OUT/bench_gather20.log 2>&1; rc=$?
