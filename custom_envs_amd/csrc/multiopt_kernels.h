@@ -767,6 +767,13 @@ namespace ce {
 // double-buffered by step parity behind one 192-thread barrier per step.
 // Same arithmetic, same operation order as multi_persist_kernel:
 // bit-identical outputs.
+// Diagnostic builds only (timing which wave bounds the step; outputs wrong):
+// bit 0 skips the info wave's work, bit 1 the rows wave's, bit 2 replaces
+// the state wave's exp10 by a copy (three-wave form), bit 3 skips the ratio
+// wave's work (four-wave form).
+#ifndef CE_MP2_DIAG
+#define CE_MP2_DIAG 0
+#endif
 struct MultiXch {
     double adj_g, adj_l, gsum, lsum, nsum, reward;
     float thn, lr, g, gp, loss, nw, nl, ng;
@@ -822,7 +829,7 @@ __global__ __launch_bounds__(192) void multi_persist2_kernel(MultiArgs a, int K,
             const float act_next = at32(a.act + (t + 1 < K ? (t + 1) * act_stride : 0), eu * P + r);
             const int s = s_prev + 1;
             const float x = act - 4.0f;
-            const float lr = static_cast<float>(exp10(static_cast<double>(x)));
+            const float lr = (CE_MP2_DIAG & 4) ? x : static_cast<float>(exp10(static_cast<double>(x)));
             const float thn = th - gc * lr;
             float g, loss;
             rosenbrock_lane<P>(thn, i, g, loss);
@@ -926,6 +933,7 @@ __global__ __launch_bounds__(192) void multi_persist2_kernel(MultiArgs a, int K,
             __syncthreads();                                // step t's results handed over
             const long long ro = t * out_step;
             const MultiXch &xi = xch[buf][lane];
+            if (CE_MP2_DIAG & 2) continue;
             const int s = xi.s;
             const bool wipe = xi.terminal != 0 && a.auto_reset;
             const float nw = xi.nw, ng = xi.ng, nl = xi.nl;
@@ -1008,6 +1016,7 @@ __global__ __launch_bounds__(192) void multi_persist2_kernel(MultiArgs a, int K,
             __syncthreads();                                // step t's results handed over
             const long long ro = t * out_step;
             const MultiXch xi = xch[buf][lane];
+            if (CE_MP2_DIAG & 1) continue;
             const int s = xi.s;
             const bool terminal = xi.terminal != 0;
             const bool wipe = terminal && a.auto_reset;
@@ -1057,6 +1066,345 @@ __global__ __launch_bounds__(192) void multi_persist2_kernel(MultiArgs a, int K,
                 }
                 at32(reinterpret_cast<float *>(reinterpret_cast<char *>(a.reward) + ro), eu * P + r) =
                     static_cast<float>(xi.reward);
+                at32(reinterpret_cast<uint8_t *>(a.done) + ro, eu * P + r) = terminal ? 1 : 0;
+            }
+        }
+        if (on) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) at32(a.sa, j * Eu * P + ep) = sa_v[j];
+        }
+    }
+}
+
+
+// The four-wave form (multi_persist4_kernel): multi_persist2_kernel's state
+// wave issued ≈380 instructions per step and bounded the step (its outputs'
+// work: the three ratios, reward, sums).  Here a fourth wave, on the fourth
+// SIMD, takes the ratios, the reward, the |.| sum and the info values of its
+// own operands (three of the seven group sums); the state wave keeps the
+// loop-carried chain (the update, the Rosenbrock pair), the raw history and
+// the exp10 of the next step's action, which fill its chain's latency.  One
+// 256-thread barrier per step; every hand-over is double-buffered by step
+// parity:
+//   state  (W0) step t between barriers t-1 and t: raw[t] out
+//   ratio  (W3) step t between barriers t and t+1: raw[t] in, xch[t] out
+//   rows / info (W1, W2) step t between barriers t+1 and t+2: xch[t] in
+// The arithmetic and its order are multi_persist_kernel's: bit-identical
+// outputs.
+struct MultiXch4 {       // what the rows and info waves take from the ratio wave
+    double nsum;
+    float thn, lr, loss, reward, nw, nl, ng;
+    float info8, info9, info10, info11, info12, info13;
+    int s, terminal;
+};
+struct MultiRaw {
+    double lsum, gsum;
+    float thn, g, loss, lr, gp, wp, lp;
+    int s, terminal;
+};
+
+template <int P, int HC>
+__global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K, long long act_stride,
+                                                            long long out_step) {
+#pragma clang fp contract(off)
+    constexpr int G = Group<P>::G;
+    constexpr int H = HC;
+    constexpr int row = 3 * H;
+    static_assert(HC > 0 && HC <= kMultiStageH, "compile-time history");
+    constexpr int span = 64 / G * P * row;
+    __shared__ __attribute__((aligned(16))) float stage[span];
+    __shared__ MultiXch4 xch[2][64];
+    __shared__ MultiRaw raw[2][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t gt = static_cast<size_t>(blockIdx.x) * 64 + lane;
+    const size_t e = gt / G;
+    const int i = static_cast<int>(gt % G);
+    const size_t E = a.E;
+    const bool env_ok = e < E;
+    const bool on = env_ok && i < P;
+    const size_t ec = env_ok ? e : 0;
+    const int ic = i < P ? i : 0;
+    const int r = P <= 10 ? ic : a.agent_row[ic];
+    const unsigned Eu = static_cast<unsigned>(E), eu = static_cast<unsigned>(ec);
+    const unsigned ep = eu * P + ic;
+    const size_t e_first = static_cast<size_t>(blockIdx.x) * 64 / G;
+    const size_t envs = e_first < E ? (E - e_first < static_cast<size_t>(64 / G) ? E - e_first
+                                                                                  : static_cast<size_t>(64 / G))
+                                    : 0;
+    const int nblk = static_cast<int>(envs) * P * row;
+
+    if (wave == 0) {
+        // ======================= state wave =======================
+        int s_prev = at32(a.step, eu);
+        const float th_init = i < P ? a.init[i] : 0.0f;
+        const float g_init = i < P ? a.init_g[i] : 0.0f, l_init = a.init_l;
+        float th = at32(a.theta, ep);
+        float gc = at32(a.grad, ep);
+        float hl_v[kRawHist], hg_v[kRawHist], hw_v[kRawHist];
+#pragma unroll
+        for (int k = 0; k < kRawHist; ++k) {
+            hl_v[k] = at32(a.hl, k * Eu + eu);
+            hg_v[k] = at32(a.hg, k * Eu * P + ep);
+            hw_v[k] = at32(a.hw, k * Eu * P + ep);
+        }
+        // lr = 10^(a - 4) (multioptlrs.py:81-87): an action's lr depends on
+        // the action alone, so step t + 1's is formed during step t
+        float lr = static_cast<float>(exp10(static_cast<double>(at32(a.act, eu * P + r) - 4.0f)));
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            const float act_next = at32(a.act + (t + 1 < K ? (t + 1) * act_stride : 0), eu * P + r);
+            const int s = s_prev + 1;
+            const float thn = th - gc * lr;
+            float g, loss;
+            rosenbrock_lane<P>(thn, i, g, loss);
+            bool terminal = s >= a.max_batches;
+            if (!terminal && loss > 1e4f) terminal = true;
+            const int slot = s % kRawHist, prev = (s - 1) % kRawHist;
+            float lp = 0.0f, gp = 0.0f, wp = 0.0f;
+            double lsum = loss, gsum = g;
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k) {
+                if (k == prev) {
+                    lp = hl_v[k];
+                    gp = hg_v[k];
+                    wp = hw_v[k];
+                }
+                if (k != slot) {
+                    lsum += hl_v[k];
+                    gsum += hg_v[k];
+                }
+            }
+            MultiRaw &ro = raw[buf][lane];
+            ro.lsum = lsum;
+            ro.gsum = gsum;
+            ro.thn = thn;
+            ro.g = g;
+            ro.loss = loss;
+            ro.lr = lr;
+            ro.gp = gp;
+            ro.wp = wp;
+            ro.lp = lp;
+            ro.s = s;
+            ro.terminal = terminal ? 1 : 0;
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k)
+                if (k == slot) {
+                    hg_v[k] = g;
+                    hw_v[k] = thn;
+                    hl_v[k] = loss;
+                }
+            if (terminal && a.auto_reset) {
+#pragma unroll
+                for (int k = 0; k < kRawHist; ++k) {
+                    hg_v[k] = k == 0 ? g_init : 0.0f;
+                    hw_v[k] = k == 0 ? th_init : 0.0f;
+                    hl_v[k] = k == 0 ? l_init : 0.0f;
+                }
+                th = th_init;
+                gc = g_init;
+                s_prev = 0;
+            } else {
+                th = thn;
+                gc = g;
+                s_prev = s;
+            }
+            lr = static_cast<float>(exp10(static_cast<double>(act_next - 4.0f)));
+            __syncthreads();                                // barrier t: raw[t] out
+        }
+        __syncthreads();                                    // barrier K
+        if (on) {
+            at32(a.theta, ep) = th;
+            at32(a.grad, ep) = gc;
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k) {
+                at32(a.hg, k * Eu * P + ep) = hg_v[k];
+                at32(a.hw, k * Eu * P + ep) = hw_v[k];
+                if (i == 0) at32(a.hl, k * Eu + eu) = hl_v[k];
+            }
+            if (i == 0) at32(a.step, eu) = s_prev;
+        }
+    } else if (wave == 3) {
+        // ======================= ratio wave =======================
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // barrier t: raw[t] in
+            if (CE_MP2_DIAG & 8) continue;
+            const MultiRaw ri = raw[buf][lane];
+            const int s = ri.s;
+            const double adj_l = ratio_fast(ri.loss, ri.lp);
+            const double adj_g = ratio_fast(ri.g, ri.gp);
+            const double adj_w = ratio_fast(ri.thn, ri.wp);
+            double reward = 1.0 - adj_l;
+            reward = reward < -100.0 ? -100.0 : (reward > 100.0 ? 100.0 : reward);
+            if (!(s >= a.max_batches) && ri.loss > 1e4f) reward -= static_cast<double>(a.max_batches - s);
+            // the info values of the ratio wave's own operands (the group sums
+            // of multi_persist_kernel, same butterfly)
+            auto mine = [&](double v) { return on ? v : 0.0; };
+            const double adjg = group_sum<G>(mine(fabs(adj_g))) / P;
+            const double gdiff = group_sum<G>(mine(fabs(static_cast<double>(ri.g) - static_cast<double>(ri.gp)))) / P;
+            const double gsum_all = group_sum<G>(mine(ri.gsum));
+            MultiXch4 &xo = xch[buf][lane];
+            xo.nsum = fabs(adj_w) + fabs(adj_g) + fabs(adj_l);
+            xo.thn = ri.thn;
+            xo.lr = ri.lr;
+            xo.loss = ri.loss;
+            xo.reward = static_cast<float>(reward);
+            xo.nw = static_cast<float>(clip100(adj_w) - 1.0);
+            xo.nl = static_cast<float>(clip100(adj_l) - 1.0);
+            xo.ng = static_cast<float>(clip100(adj_g) - 1.0);
+            xo.info8 = static_cast<float>(gsum_all / (kRawHist * P));
+            xo.info9 = static_cast<float>(gsum_all);
+            xo.info10 = static_cast<float>(ri.lsum / kRawHist);
+            xo.info11 = static_cast<float>(adj_l);
+            xo.info12 = static_cast<float>(adjg);
+            xo.info13 = static_cast<float>(gdiff);
+            xo.s = s;
+            xo.terminal = ri.terminal;
+        }
+        __syncthreads();                                    // barrier K
+    } else if (wave == 1) {
+        // ======================= rows wave =======================
+        float ol_v[H], og_v[H], ow_v[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            ol_v[j] = at32(a.ol, j * Eu + eu);
+            og_v[j] = at32(a.og, j * Eu * P + ep);
+            ow_v[j] = at32(a.ow, j * Eu * P + ep);
+        }
+        float *const lrow = stage + ((lane / G) * P + r) * row;
+        __syncthreads();                                    // barrier 0
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // barrier t + 1: xch[t] in
+            const long long ro = t * out_step;
+            const MultiXch4 &xi = xch[buf][lane];
+            if (CE_MP2_DIAG & 2) continue;
+            const int s = xi.s;
+            const bool wipe = xi.terminal != 0 && a.auto_reset;
+            const float nw = xi.nw, ng = xi.ng, nl = xi.nl;
+            const int aslot = (s - 1) % H;
+            const int k0 = aslot;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const int kk = k0 - j >= 0 ? k0 - j : k0 - j + H;
+                float wk = ow_v[j], gk = og_v[j], lk = ol_v[j];
+                if (kk == 0) {
+                    wk = nw;
+                    gk = ng;
+                    lk = nl;
+                }
+                if (on) {
+                    lrow[kk] = wipe ? -1.0f : wk;
+                    lrow[H + kk] = wipe ? -1.0f : lk;
+                    lrow[2 * H + kk] = wipe ? -1.0f : gk;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+                if (j == aslot) {
+                    og_v[j] = ng;
+                    ow_v[j] = nw;
+                    ol_v[j] = nl;
+                }
+            if (wipe) {
+#pragma unroll
+                for (int j = 0; j < H; ++j) {
+                    og_v[j] = -1.0f;
+                    ow_v[j] = -1.0f;
+                    ol_v[j] = -1.0f;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            {
+                const float *lds = stage;
+                float *out = reinterpret_cast<float *>(reinterpret_cast<char *>(a.obs) + ro) + e_first * P * row;
+                constexpr int kV = (span / 4 + 63) / 64;
+                if ((nblk & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+                    const float4 *src = reinterpret_cast<const float4 *>(lds);
+                    float4 *dst4 = reinterpret_cast<float4 *>(out);
+                    const int n4 = nblk >> 2;
+                    float4 v[kV];
+#pragma unroll
+                    for (int u = 0; u < kV; ++u) {
+                        const int q = lane + 64 * u;
+                        v[u] = src[q < n4 ? q : n4 - 1];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kV; ++u) {
+                        const int q = lane + 64 * u;
+                        if (q < n4) dst4[q] = v[u];
+                    }
+                } else {
+                    for (int q = lane; q < nblk; q += 64) out[q] = lds[q];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (on) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                at32(a.og, j * Eu * P + ep) = og_v[j];
+                at32(a.ow, j * Eu * P + ep) = ow_v[j];
+                if (i == 0) at32(a.ol, j * Eu + eu) = ol_v[j];
+            }
+        }
+    } else {
+        // ======================= info wave =======================
+        double sa_v[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) sa_v[j] = at32(a.sa, j * Eu * P + ep);
+        __syncthreads();                                    // barrier 0
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // barrier t + 1: xch[t] in
+            const long long ro = t * out_step;
+            const MultiXch4 xi = xch[buf][lane];
+            if (CE_MP2_DIAG & 1) continue;
+            const int s = xi.s;
+            const bool terminal = xi.terminal != 0;
+            const bool wipe = terminal && a.auto_reset;
+            const int aslot = (s - 1) % H;
+            double st_abs = 0.0;
+            const int k0 = aslot;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const int kk = k0 - j >= 0 ? k0 - j : k0 - j + H;
+                st_abs += kk == 0 ? xi.nsum : sa_v[j];
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+                if (j == aslot) sa_v[j] = xi.nsum;
+            if (wipe) {
+#pragma unroll
+                for (int j = 0; j < H; ++j) sa_v[j] = 0.0;
+            }
+            const double thn = xi.thn, lr = xi.lr;
+            auto mine = [&](double v) { return on ? v : 0.0; };
+            const double wsum = group_sum<G>(mine(fabs(thn)));
+            const double amean = group_sum<G>(mine(lr)) / P;
+            const double dev = lr - amean;
+            const double avar = group_sum<G>(mine(dev * dev)) / P;
+            const double st_all = group_sum<G>(mine(st_abs));
+            if (on) {
+                if (i == 0) {
+                    float *info = reinterpret_cast<float *>(reinterpret_cast<char *>(a.info) + ro) + eu * kMultiInfo;
+                    info[0] = terminal ? xi.loss : __builtin_nanf("");
+                    info[1] = xi.loss;
+                    info[2] = static_cast<float>(wsum / P);
+                    info[3] = static_cast<float>(wsum);
+                    info[4] = static_cast<float>(amean);
+                    info[5] = static_cast<float>(sqrt(avar));
+                    info[6] = static_cast<float>(st_all / (P * row));
+                    info[7] = static_cast<float>(st_all);
+                    info[8] = xi.info8;
+                    info[9] = xi.info9;
+                    info[10] = xi.info10;
+                    info[11] = xi.info11;
+                    info[12] = xi.info12;
+                    info[13] = xi.info13;
+                    at32(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro), eu) = xi.s;
+                }
+                at32(reinterpret_cast<float *>(reinterpret_cast<char *>(a.reward) + ro), eu * P + r) = xi.reward;
                 at32(reinterpret_cast<uint8_t *>(a.done) + ro, eu * P + r) = terminal ? 1 : 0;
             }
         }
