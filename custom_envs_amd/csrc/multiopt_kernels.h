@@ -1081,9 +1081,11 @@ __global__ __launch_bounds__(192) void multi_persist2_kernel(MultiArgs a, int K,
 // wave issued ≈380 instructions per step and bounded the step (its outputs'
 // work: the three ratios, reward, sums).  Here a fourth wave, on the fourth
 // SIMD, takes the ratios, the reward, the |.| sum and the info values of its
-// own operands (three of the seven group sums); the state wave keeps the
-// loop-carried chain (the update, the Rosenbrock pair), the raw history and
-// the exp10 of the next step's action, which fill its chain's latency.  One
+// own operands (two of the seven group sums); the state wave keeps the
+// loop-carried chain (the update, the Rosenbrock pair), the raw history, its
+// sums' info values and the exp10 of the next step's action, which fill its
+// chain's latency.  The rows wave holds its rings newest first (a shift
+// register), so the rows are written at constant LDS offsets.  One
 // 256-thread barrier per step; every hand-over is double-buffered by step
 // parity:
 //   state  (W0) step t between barriers t-1 and t: raw[t] out
@@ -1098,8 +1100,8 @@ struct MultiXch4 {       // what the rows and info waves take from the ratio wav
     int s, terminal;
 };
 struct MultiRaw {
-    double lsum, gsum;
     float thn, g, loss, lr, gp, wp, lp;
+    float info8, info9, info10;
     int s, terminal;
 };
 
@@ -1115,6 +1117,7 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
     __shared__ __attribute__((aligned(16))) float stage[span];
     __shared__ MultiXch4 xch[2][64];
     __shared__ MultiRaw raw[2][64];
+    // (the wave index made wave-uniform by readfirstlane measured 2 % slower)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t gt = static_cast<size_t>(blockIdx.x) * 64 + lane;
     const size_t e = gt / G;
@@ -1174,9 +1177,12 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
                     gsum += hg_v[k];
                 }
             }
+            // the raw sums' info values (the state wave has the slack)
+            const double gsum_all = group_sum<G>(on ? gsum : 0.0);
             MultiRaw &ro = raw[buf][lane];
-            ro.lsum = lsum;
-            ro.gsum = gsum;
+            ro.info8 = static_cast<float>(gsum_all / (kRawHist * P));
+            ro.info9 = static_cast<float>(gsum_all);
+            ro.info10 = static_cast<float>(lsum / kRawHist);
             ro.thn = thn;
             ro.g = g;
             ro.loss = loss;
@@ -1242,7 +1248,6 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
             auto mine = [&](double v) { return on ? v : 0.0; };
             const double adjg = group_sum<G>(mine(fabs(adj_g))) / P;
             const double gdiff = group_sum<G>(mine(fabs(static_cast<double>(ri.g) - static_cast<double>(ri.gp)))) / P;
-            const double gsum_all = group_sum<G>(mine(ri.gsum));
             MultiXch4 &xo = xch[buf][lane];
             xo.nsum = fabs(adj_w) + fabs(adj_g) + fabs(adj_l);
             xo.thn = ri.thn;
@@ -1252,9 +1257,9 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
             xo.nw = static_cast<float>(clip100(adj_w) - 1.0);
             xo.nl = static_cast<float>(clip100(adj_l) - 1.0);
             xo.ng = static_cast<float>(clip100(adj_g) - 1.0);
-            xo.info8 = static_cast<float>(gsum_all / (kRawHist * P));
-            xo.info9 = static_cast<float>(gsum_all);
-            xo.info10 = static_cast<float>(ri.lsum / kRawHist);
+            xo.info8 = ri.info8;
+            xo.info9 = ri.info9;
+            xo.info10 = ri.info10;
             xo.info11 = static_cast<float>(adj_l);
             xo.info12 = static_cast<float>(adjg);
             xo.info13 = static_cast<float>(gdiff);
@@ -1264,14 +1269,22 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
         __syncthreads();                                    // barrier K
     } else if (wave == 1) {
         // ======================= rows wave =======================
+        // The adjusted rings' observation columns, held newest first (a
+        // shift register: the row is the ring as it stands, written at
+        // constant LDS offsets).  In HBM they stay in slot order, slot
+        // (s - 1) % H the newest, as the one-step kernel keeps them.
+        const int s0 = at32(a.step, eu);
+        const int new0 = ((s0 - 1) % H + H) % H;
         float ol_v[H], og_v[H], ow_v[H];
 #pragma unroll
-        for (int j = 0; j < H; ++j) {
-            ol_v[j] = at32(a.ol, j * Eu + eu);
-            og_v[j] = at32(a.og, j * Eu * P + ep);
-            ow_v[j] = at32(a.ow, j * Eu * P + ep);
+        for (int q = 0; q < H; ++q) {
+            const int j = (new0 - q + H) % H;
+            ol_v[q] = at32(a.ol, j * Eu + eu);
+            og_v[q] = at32(a.og, j * Eu * P + ep);
+            ow_v[q] = at32(a.ow, j * Eu * P + ep);
         }
         float *const lrow = stage + ((lane / G) * P + r) * row;
+        int s_end = s0;
         __syncthreads();                                    // barrier 0
         for (int t = 0; t < K; ++t) {
             const int buf = t & 1;
@@ -1279,39 +1292,32 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
             const long long ro = t * out_step;
             const MultiXch4 &xi = xch[buf][lane];
             if (CE_MP2_DIAG & 2) continue;
-            const int s = xi.s;
             const bool wipe = xi.terminal != 0 && a.auto_reset;
             const float nw = xi.nw, ng = xi.ng, nl = xi.nl;
-            const int aslot = (s - 1) % H;
-            const int k0 = aslot;
+            s_end = wipe ? 0 : xi.s;
 #pragma unroll
-            for (int j = 0; j < H; ++j) {
-                const int kk = k0 - j >= 0 ? k0 - j : k0 - j + H;
-                float wk = ow_v[j], gk = og_v[j], lk = ol_v[j];
-                if (kk == 0) {
-                    wk = nw;
-                    gk = ng;
-                    lk = nl;
-                }
-                if (on) {
-                    lrow[kk] = wipe ? -1.0f : wk;
-                    lrow[H + kk] = wipe ? -1.0f : lk;
-                    lrow[2 * H + kk] = wipe ? -1.0f : gk;
-                }
+            for (int q = H - 1; q > 0; --q) {
+                og_v[q] = og_v[q - 1];
+                ow_v[q] = ow_v[q - 1];
+                ol_v[q] = ol_v[q - 1];
             }
-#pragma unroll
-            for (int j = 0; j < H; ++j)
-                if (j == aslot) {
-                    og_v[j] = ng;
-                    ow_v[j] = nw;
-                    ol_v[j] = nl;
-                }
+            og_v[0] = ng;
+            ow_v[0] = nw;
+            ol_v[0] = nl;
             if (wipe) {
 #pragma unroll
-                for (int j = 0; j < H; ++j) {
-                    og_v[j] = -1.0f;
-                    ow_v[j] = -1.0f;
-                    ol_v[j] = -1.0f;
+                for (int q = 0; q < H; ++q) {
+                    og_v[q] = -1.0f;
+                    ow_v[q] = -1.0f;
+                    ol_v[q] = -1.0f;
+                }
+            }
+            if (on) {
+#pragma unroll
+                for (int q = 0; q < H; ++q) {
+                    lrow[q] = ow_v[q];
+                    lrow[H + q] = ol_v[q];
+                    lrow[2 * H + q] = og_v[q];
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -1341,11 +1347,13 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
             __builtin_amdgcn_wave_barrier();
         }
         if (on) {
+            const int new_end = ((s_end - 1) % H + H) % H;
 #pragma unroll
-            for (int j = 0; j < H; ++j) {
-                at32(a.og, j * Eu * P + ep) = og_v[j];
-                at32(a.ow, j * Eu * P + ep) = ow_v[j];
-                if (i == 0) at32(a.ol, j * Eu + eu) = ol_v[j];
+            for (int q = 0; q < H; ++q) {
+                const int j = (new_end - q + H) % H;
+                at32(a.og, j * Eu * P + ep) = og_v[q];
+                at32(a.ow, j * Eu * P + ep) = ow_v[q];
+                if (i == 0) at32(a.ol, j * Eu + eu) = ol_v[q];
             }
         }
     } else {
@@ -1378,9 +1386,9 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
 #pragma unroll
                 for (int j = 0; j < H; ++j) sa_v[j] = 0.0;
             }
-            const double thn = xi.thn, lr = xi.lr;
+            const double lr = xi.lr;
             auto mine = [&](double v) { return on ? v : 0.0; };
-            const double wsum = group_sum<G>(mine(fabs(thn)));
+            const double wsum = group_sum<G>(mine(fabs(static_cast<double>(xi.thn))));
             const double amean = group_sum<G>(mine(lr)) / P;
             const double dev = lr - amean;
             const double avar = group_sum<G>(mine(dev * dev)) / P;
@@ -1392,6 +1400,7 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
                     info[1] = xi.loss;
                     info[2] = static_cast<float>(wsum / P);
                     info[3] = static_cast<float>(wsum);
+                    at32(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro), eu) = xi.s;
                     info[4] = static_cast<float>(amean);
                     info[5] = static_cast<float>(sqrt(avar));
                     info[6] = static_cast<float>(st_all / (P * row));
@@ -1402,7 +1411,6 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
                     info[11] = xi.info11;
                     info[12] = xi.info12;
                     info[13] = xi.info13;
-                    at32(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro), eu) = xi.s;
                 }
                 at32(reinterpret_cast<float *>(reinterpret_cast<char *>(a.reward) + ro), eu * P + r) = xi.reward;
                 at32(reinterpret_cast<uint8_t *>(a.done) + ro, eu * P + r) = terminal ? 1 : 0;
