@@ -413,6 +413,53 @@ def test_persistent_multi_bit_equal_to_step_launches(problem, E, MB, T, chunks):
         assert np.array_equal(sa[name], sb[name]), name
 
 
+def test_persistent_and_step_launches_interleaved():
+    """The K-step kernel and the one-step kernel share the state's HBM layout
+    (the history rings in slot order, slot (s - 1) % H the newest; the K-step
+    kernel's rows wave holds them newest first and maps at each launch end):
+    a rollout that switches between them every few steps, at every ring
+    phase, gives the pure one-step rollout's bits."""
+    from custom_envs_amd.multi_engine import MultiOptEngine
+    E, MB, T = 96, 23, 60
+    plan = [(True, 7), (False, 3), (True, 11), (False, 2), (True, 1), (False, 4),
+            (True, 9), (False, 1), (True, 13), (False, 9)]
+    assert sum(k for _, k in plan) == T
+    res = []
+    for mixed in (False, True):
+        eng = MultiOptEngine(E, 'func4', max_batches=MB, max_history=5)
+        P = eng.n_params
+        acts = np.random.RandomState(5).uniform(1.0, 2.6, (T, E * P)).astype(np.float32)
+        if mixed:
+            import torch
+            stream = torch.cuda.Stream()
+            rec = {}
+            with torch.cuda.stream(stream):
+                eng.set_stream(stream.cuda_stream)
+                eng.reset_device(eng.alloc_device_outputs())
+                dact = torch.from_numpy(acts).cuda()
+                t = 0
+                for persist, k in plan:
+                    eng.set_persistent(persist)
+                    fields, rb = eng.alloc_rollout(k)
+                    eng.rollout_device(k, dact[t:t + k].contiguous(), fields, rb)
+                    stream.synchronize()
+                    for name, v in fields.items():
+                        if name != '_buffer':
+                            rec.setdefault(name, []).append(v.cpu().numpy())
+                    t += k
+            res.append(({k: np.concatenate(v) for k, v in rec.items()}, eng.get_state()))
+        else:
+            eng.set_persistent(False)
+            res.append(_multi_rollout(eng, acts, [T]))
+        eng.close()
+    (a, sa), (b, sb) = res
+    for name in a:
+        assert np.array_equal(a[name], b[name], equal_nan=True), name
+    assert a['done'].any(), 'no episode ended'
+    for name in ('theta', 'step'):
+        assert np.array_equal(sa[name], sb[name]), name
+
+
 def test_persistent_multi_against_oracle():
     """The persistent kernel against live oracle runners: 64 envs x 4 agents,
     mixed stable / divergent action ranges, max_batches 30 over 70 steps in
