@@ -389,6 +389,10 @@ def _multi_rollout(eng, acts, chunks):
     ('func4', 1024, 400, 45, [20, 20, 5]),      # config 5's shape; loss > 1e4 stops
     ('func4', 77, 9, 40, [13, 1, 26]),           # max_batches ends, a partial last wave
     ({'ndims': 6, 'initial_points': [-1.9, 2.0, -1.0, 1.5, 0.5, -0.5]}, 40, 12, 30, [30]),  # idle lanes
+    # 16-lane groups (P = 12: idle lanes; P = 16: full) and the agent-row
+    # indirection of P > 10, across ring phases (chunks of 7, 3, 11)
+    ({'ndims': 12, 'initial_points': [(-1.0) ** i * (0.25 + 0.1 * i) for i in range(12)]}, 33, 10, 21, [7, 3, 11]),
+    ({'ndims': 16, 'initial_points': [(-1.0) ** i * (0.3 + 0.05 * i) for i in range(16)]}, 20, 8, 21, [7, 3, 11]),
 ])
 def test_persistent_multi_bit_equal_to_step_launches(problem, E, MB, T, chunks):
     """multi_persist_kernel (K steps per launch, the state in registers) gives
