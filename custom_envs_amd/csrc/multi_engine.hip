@@ -45,14 +45,16 @@ void launch_multi_step(const ce::MultiArgs &a, int, hipStream_t s) {
 }
 // K steps in one launch (multi_persist_kernel): the reference default history
 // H = 5 only (the compile-time instance the kernel needs)
-// the split forms: four waves (state, ratio, rows, info; the default), three
+// the split forms: five waves (state, sums, ratio, rows, info; the default),
+// four (CE_MULTI_FORM=four: the state wave keeps the raw history), three
 // (CE_MULTI_FORM=three: state, rows, info) or one (CE_MULTI_FORM=one), A/B
 int multi_form() {
     static const int form = [] {
         const char *v = std::getenv("CE_MULTI_FORM");
         if (v && std::strcmp(v, "one") == 0) return 1;
         if (v && std::strcmp(v, "three") == 0) return 3;
-        return 4;
+        if (v && std::strcmp(v, "four") == 0) return 4;
+        return 5;
     }();
     return form;
 }
@@ -61,6 +63,11 @@ void launch_multi_persist(const ce::MultiArgs &a, int k, long long act_stride, l
                           hipStream_t s) {
     const long lanes = static_cast<long>(a.E) * ce::Group<P>::G;
     const dim3 grid(static_cast<int>((lanes + 63) / 64));
+    if (multi_form() == 5) {
+        hipLaunchKernelGGL((ce::multi_persist5_kernel<P, 5>), grid, dim3(320), 0, s, a, k, act_stride,
+                           out_step);
+        return;
+    }
     if (multi_form() == 4) {
         hipLaunchKernelGGL((ce::multi_persist4_kernel<P, 5>), grid, dim3(256), 0, s, a, k, act_stride,
                            out_step);
@@ -246,7 +253,8 @@ int ce_multi_create(const ce_multi_config *cfg, ce_multi_engine **out) {
     if (const char *pe = std::getenv("CE_PERSIST")) e->persist_on = pe[0] != '0';
     e->step_name = "multi_step_kernel<" + std::to_string(cfg->n_params) + "," +
                    std::to_string(cfg->max_history == 5 ? 5 : 0) + ">";
-    e->many_name = std::string(multi_form() == 4   ? "multi_persist4_kernel<"
+    e->many_name = std::string(multi_form() == 5   ? "multi_persist5_kernel<"
+                               : multi_form() == 4 ? "multi_persist4_kernel<"
                                : multi_form() == 3 ? "multi_persist2_kernel<"
                                                    : "multi_persist_kernel<") +
                    std::to_string(cfg->n_params) + ",5>";

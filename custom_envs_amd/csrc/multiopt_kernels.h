@@ -1423,4 +1423,370 @@ __global__ __launch_bounds__(256) void multi_persist4_kernel(MultiArgs a, int K,
     }
 }
 
+// The five-wave form (multi_persist5_kernel, the default; CE_MULTI_FORM=four
+// runs the four-wave form): the four-wave state wave's raw history and sums
+// move to a fifth wave (sharing SIMD 0 with the state wave), so the state
+// wave issues only its chain (≈80 instructions per step): the update, the
+// Rosenbrock pair, the terminal test and the next lr.  One more pipeline
+// stage: state step t between barriers t-1 and t, sums between t and t+1,
+// ratio between t+1 and t+2, rows / info between t+2 and t+3; K + 2
+// barriers per launch.  Measured 0.59 -> 0.525 us per 1024-env step long
+// run, 1.38 -> 1.30-1.32 in the driver form (profiles/r06q_*).
+// The sums wave is wave 4 (with the state wave's SIMD if waves pair round
+// robin); the rows wave there instead measured 0.530 against 0.525 us per
+// step (profiles/r06s_*)
+constexpr int kSumsWave = 4;
+constexpr int kRowsWave = 1;
+struct MultiRaw0 {       // what the sums wave takes from the state wave
+    float thn, g, loss, lr;
+    int s, terminal;
+};
+
+template <int P, int HC>
+__global__ __launch_bounds__(320) void multi_persist5_kernel(MultiArgs a, int K, long long act_stride,
+                                                            long long out_step) {
+#pragma clang fp contract(off)
+    constexpr int G = Group<P>::G;
+    constexpr int H = HC;
+    constexpr int row = 3 * H;
+    static_assert(HC > 0 && HC <= kMultiStageH, "compile-time history");
+    constexpr int span = 64 / G * P * row;
+    __shared__ __attribute__((aligned(16))) float stage[span];
+    __shared__ MultiXch4 xch[2][64];
+    __shared__ MultiRaw raw[2][64];         // sums wave -> ratio wave
+    __shared__ MultiRaw0 raw0[2][64];       // state wave -> sums wave
+    // (the wave index made wave-uniform by readfirstlane measured 2 % slower)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t gt = static_cast<size_t>(blockIdx.x) * 64 + lane;
+    const size_t e = gt / G;
+    const int i = static_cast<int>(gt % G);
+    const size_t E = a.E;
+    const bool env_ok = e < E;
+    const bool on = env_ok && i < P;
+    const size_t ec = env_ok ? e : 0;
+    const int ic = i < P ? i : 0;
+    const int r = P <= 10 ? ic : a.agent_row[ic];
+    const unsigned Eu = static_cast<unsigned>(E), eu = static_cast<unsigned>(ec);
+    const unsigned ep = eu * P + ic;
+    const size_t e_first = static_cast<size_t>(blockIdx.x) * 64 / G;
+    const size_t envs = e_first < E ? (E - e_first < static_cast<size_t>(64 / G) ? E - e_first
+                                                                                  : static_cast<size_t>(64 / G))
+                                    : 0;
+    const int nblk = static_cast<int>(envs) * P * row;
+
+    if (wave == 0) {
+        // ======================= state wave =======================
+        // the loop-carried chain only: the update, the Rosenbrock pair, the
+        // terminal test; lr of the next step's action beside it
+        int s_prev = at32(a.step, eu);
+        const float th_init = i < P ? a.init[i] : 0.0f;
+        const float g_init = i < P ? a.init_g[i] : 0.0f;
+        float th = at32(a.theta, ep);
+        float gc = at32(a.grad, ep);
+        float lr = static_cast<float>(exp10(static_cast<double>(at32(a.act, eu * P + r) - 4.0f)));
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            const float act_next = at32(a.act + (t + 1 < K ? (t + 1) * act_stride : 0), eu * P + r);
+            const int s = s_prev + 1;
+            const float thn = th - gc * lr;
+            float g, loss;
+            rosenbrock_lane<P>(thn, i, g, loss);
+            bool terminal = s >= a.max_batches;
+            if (!terminal && loss > 1e4f) terminal = true;
+            MultiRaw0 &ro = raw0[buf][lane];
+            ro.thn = thn;
+            ro.g = g;
+            ro.loss = loss;
+            ro.lr = lr;
+            ro.s = s;
+            ro.terminal = terminal ? 1 : 0;
+            if (terminal && a.auto_reset) {
+                th = th_init;
+                gc = g_init;
+                s_prev = 0;
+            } else {
+                th = thn;
+                gc = g;
+                s_prev = s;
+            }
+            lr = static_cast<float>(exp10(static_cast<double>(act_next - 4.0f)));
+            __syncthreads();                                // barrier t: raw0[t] out
+        }
+        __syncthreads();                                    // barrier K
+        __syncthreads();                                    // barrier K + 1
+        if (on) {
+            at32(a.theta, ep) = th;
+            at32(a.grad, ep) = gc;
+            if (i == 0) at32(a.step, eu) = s_prev;
+        }
+    } else if (wave == kSumsWave) {
+        // ======================= sums wave =======================
+        // the raw history, the previous entries and the raw sums' info values
+        const float th_init = i < P ? a.init[i] : 0.0f;
+        const float g_init = i < P ? a.init_g[i] : 0.0f, l_init = a.init_l;
+        float hl_v[kRawHist], hg_v[kRawHist], hw_v[kRawHist];
+#pragma unroll
+        for (int k = 0; k < kRawHist; ++k) {
+            hl_v[k] = at32(a.hl, k * Eu + eu);
+            hg_v[k] = at32(a.hg, k * Eu * P + ep);
+            hw_v[k] = at32(a.hw, k * Eu * P + ep);
+        }
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // barrier t: raw0[t] in
+            const MultiRaw0 ri = raw0[buf][lane];
+            const int s = ri.s;
+            const float thn = ri.thn, g = ri.g, loss = ri.loss;
+            const int slot = s % kRawHist, prev = (s - 1) % kRawHist;
+            float lp = 0.0f, gp = 0.0f, wp = 0.0f;
+            double lsum = loss, gsum = g;
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k) {
+                if (k == prev) {
+                    lp = hl_v[k];
+                    gp = hg_v[k];
+                    wp = hw_v[k];
+                }
+                if (k != slot) {
+                    lsum += hl_v[k];
+                    gsum += hg_v[k];
+                }
+            }
+            const double gsum_all = group_sum<G>(on ? gsum : 0.0);
+            MultiRaw &ro = raw[buf][lane];
+            ro.info8 = static_cast<float>(gsum_all / (kRawHist * P));
+            ro.info9 = static_cast<float>(gsum_all);
+            ro.info10 = static_cast<float>(lsum / kRawHist);
+            ro.thn = thn;
+            ro.g = g;
+            ro.loss = loss;
+            ro.lr = ri.lr;
+            ro.gp = gp;
+            ro.wp = wp;
+            ro.lp = lp;
+            ro.s = s;
+            ro.terminal = ri.terminal;
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k)
+                if (k == slot) {
+                    hg_v[k] = g;
+                    hw_v[k] = thn;
+                    hl_v[k] = loss;
+                }
+            if (ri.terminal && a.auto_reset) {
+#pragma unroll
+                for (int k = 0; k < kRawHist; ++k) {
+                    hg_v[k] = k == 0 ? g_init : 0.0f;
+                    hw_v[k] = k == 0 ? th_init : 0.0f;
+                    hl_v[k] = k == 0 ? l_init : 0.0f;
+                }
+            }
+        }
+        __syncthreads();                                    // barrier K
+        __syncthreads();                                    // barrier K + 1
+        if (on) {
+#pragma unroll
+            for (int k = 0; k < kRawHist; ++k) {
+                at32(a.hg, k * Eu * P + ep) = hg_v[k];
+                at32(a.hw, k * Eu * P + ep) = hw_v[k];
+                if (i == 0) at32(a.hl, k * Eu + eu) = hl_v[k];
+            }
+        }
+    } else if (wave == 3) {
+        // ======================= ratio wave =======================
+        __syncthreads();                                    // barrier 0
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // barrier t + 1: raw[t] in
+            if (CE_MP2_DIAG & 8) continue;
+            const MultiRaw ri = raw[buf][lane];
+            const int s = ri.s;
+            const double adj_l = ratio_fast(ri.loss, ri.lp);
+            const double adj_g = ratio_fast(ri.g, ri.gp);
+            const double adj_w = ratio_fast(ri.thn, ri.wp);
+            double reward = 1.0 - adj_l;
+            reward = reward < -100.0 ? -100.0 : (reward > 100.0 ? 100.0 : reward);
+            if (!(s >= a.max_batches) && ri.loss > 1e4f) reward -= static_cast<double>(a.max_batches - s);
+            // the info values of the ratio wave's own operands (the group sums
+            // of multi_persist_kernel, same butterfly)
+            auto mine = [&](double v) { return on ? v : 0.0; };
+            const double adjg = group_sum<G>(mine(fabs(adj_g))) / P;
+            const double gdiff = group_sum<G>(mine(fabs(static_cast<double>(ri.g) - static_cast<double>(ri.gp)))) / P;
+            MultiXch4 &xo = xch[buf][lane];
+            xo.nsum = fabs(adj_w) + fabs(adj_g) + fabs(adj_l);
+            xo.thn = ri.thn;
+            xo.lr = ri.lr;
+            xo.loss = ri.loss;
+            xo.reward = static_cast<float>(reward);
+            xo.nw = static_cast<float>(clip100(adj_w) - 1.0);
+            xo.nl = static_cast<float>(clip100(adj_l) - 1.0);
+            xo.ng = static_cast<float>(clip100(adj_g) - 1.0);
+            xo.info8 = ri.info8;
+            xo.info9 = ri.info9;
+            xo.info10 = ri.info10;
+            xo.info11 = static_cast<float>(adj_l);
+            xo.info12 = static_cast<float>(adjg);
+            xo.info13 = static_cast<float>(gdiff);
+            xo.s = s;
+            xo.terminal = ri.terminal;
+        }
+        __syncthreads();                                    // barrier K + 1
+    } else if (wave == kRowsWave) {
+        // ======================= rows wave =======================
+        // The adjusted rings' observation columns, held newest first (a
+        // shift register: the row is the ring as it stands, written at
+        // constant LDS offsets).  In HBM they stay in slot order, slot
+        // (s - 1) % H the newest, as the one-step kernel keeps them.
+        const int s0 = at32(a.step, eu);
+        const int new0 = ((s0 - 1) % H + H) % H;
+        float ol_v[H], og_v[H], ow_v[H];
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+            const int j = (new0 - q + H) % H;
+            ol_v[q] = at32(a.ol, j * Eu + eu);
+            og_v[q] = at32(a.og, j * Eu * P + ep);
+            ow_v[q] = at32(a.ow, j * Eu * P + ep);
+        }
+        float *const lrow = stage + ((lane / G) * P + r) * row;
+        int s_end = s0;
+        __syncthreads();                                    // barrier 0
+        __syncthreads();                                    // barrier 1
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // barrier t + 2: xch[t] in
+            const long long ro = t * out_step;
+            const MultiXch4 &xi = xch[buf][lane];
+            if (CE_MP2_DIAG & 2) continue;
+            const bool wipe = xi.terminal != 0 && a.auto_reset;
+            const float nw = xi.nw, ng = xi.ng, nl = xi.nl;
+            s_end = wipe ? 0 : xi.s;
+#pragma unroll
+            for (int q = H - 1; q > 0; --q) {
+                og_v[q] = og_v[q - 1];
+                ow_v[q] = ow_v[q - 1];
+                ol_v[q] = ol_v[q - 1];
+            }
+            og_v[0] = ng;
+            ow_v[0] = nw;
+            ol_v[0] = nl;
+            if (wipe) {
+#pragma unroll
+                for (int q = 0; q < H; ++q) {
+                    og_v[q] = -1.0f;
+                    ow_v[q] = -1.0f;
+                    ol_v[q] = -1.0f;
+                }
+            }
+            if (on) {
+#pragma unroll
+                for (int q = 0; q < H; ++q) {
+                    lrow[q] = ow_v[q];
+                    lrow[H + q] = ol_v[q];
+                    lrow[2 * H + q] = og_v[q];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            {
+                const float *lds = stage;
+                float *out = reinterpret_cast<float *>(reinterpret_cast<char *>(a.obs) + ro) + e_first * P * row;
+                constexpr int kV = (span / 4 + 63) / 64;
+                if ((nblk & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+                    const float4 *src = reinterpret_cast<const float4 *>(lds);
+                    float4 *dst4 = reinterpret_cast<float4 *>(out);
+                    const int n4 = nblk >> 2;
+                    float4 v[kV];
+#pragma unroll
+                    for (int u = 0; u < kV; ++u) {
+                        const int q = lane + 64 * u;
+                        v[u] = src[q < n4 ? q : n4 - 1];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kV; ++u) {
+                        const int q = lane + 64 * u;
+                        if (q < n4) dst4[q] = v[u];
+                    }
+                } else {
+                    for (int q = lane; q < nblk; q += 64) out[q] = lds[q];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (on) {
+            const int new_end = ((s_end - 1) % H + H) % H;
+#pragma unroll
+            for (int q = 0; q < H; ++q) {
+                const int j = (new_end - q + H) % H;
+                at32(a.og, j * Eu * P + ep) = og_v[q];
+                at32(a.ow, j * Eu * P + ep) = ow_v[q];
+                if (i == 0) at32(a.ol, j * Eu + eu) = ol_v[q];
+            }
+        }
+    } else {
+        // ======================= info wave =======================
+        double sa_v[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) sa_v[j] = at32(a.sa, j * Eu * P + ep);
+        __syncthreads();                                    // barrier 0
+        __syncthreads();                                    // barrier 1
+        for (int t = 0; t < K; ++t) {
+            const int buf = t & 1;
+            __syncthreads();                                // barrier t + 2: xch[t] in
+            const long long ro = t * out_step;
+            const MultiXch4 xi = xch[buf][lane];
+            if (CE_MP2_DIAG & 1) continue;
+            const int s = xi.s;
+            const bool terminal = xi.terminal != 0;
+            const bool wipe = terminal && a.auto_reset;
+            const int aslot = (s - 1) % H;
+            double st_abs = 0.0;
+            const int k0 = aslot;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const int kk = k0 - j >= 0 ? k0 - j : k0 - j + H;
+                st_abs += kk == 0 ? xi.nsum : sa_v[j];
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+                if (j == aslot) sa_v[j] = xi.nsum;
+            if (wipe) {
+#pragma unroll
+                for (int j = 0; j < H; ++j) sa_v[j] = 0.0;
+            }
+            const double lr = xi.lr;
+            auto mine = [&](double v) { return on ? v : 0.0; };
+            const double wsum = group_sum<G>(mine(fabs(static_cast<double>(xi.thn))));
+            const double amean = group_sum<G>(mine(lr)) / P;
+            const double dev = lr - amean;
+            const double avar = group_sum<G>(mine(dev * dev)) / P;
+            const double st_all = group_sum<G>(mine(st_abs));
+            if (on) {
+                if (i == 0) {
+                    float *info = reinterpret_cast<float *>(reinterpret_cast<char *>(a.info) + ro) + eu * kMultiInfo;
+                    info[0] = terminal ? xi.loss : __builtin_nanf("");
+                    info[1] = xi.loss;
+                    info[2] = static_cast<float>(wsum / P);
+                    info[3] = static_cast<float>(wsum);
+                    at32(reinterpret_cast<int32_t *>(reinterpret_cast<char *>(a.episode_len) + ro), eu) = xi.s;
+                    info[4] = static_cast<float>(amean);
+                    info[5] = static_cast<float>(sqrt(avar));
+                    info[6] = static_cast<float>(st_all / (P * row));
+                    info[7] = static_cast<float>(st_all);
+                    info[8] = xi.info8;
+                    info[9] = xi.info9;
+                    info[10] = xi.info10;
+                    info[11] = xi.info11;
+                    info[12] = xi.info12;
+                    info[13] = xi.info13;
+                }
+                at32(reinterpret_cast<float *>(reinterpret_cast<char *>(a.reward) + ro), eu * P + r) = xi.reward;
+                at32(reinterpret_cast<uint8_t *>(a.done) + ro, eu * P + r) = terminal ? 1 : 0;
+            }
+        }
+        if (on) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) at32(a.sa, j * Eu * P + ep) = sa_v[j];
+        }
+    }
+}
+
 }  // namespace ce

@@ -475,7 +475,7 @@ def test_persistent_multi_against_oracle():
     actions = np.stack([rs.uniform(lows[e], lows[e] + 1.5, (T, P)) for e in range(E)], 1)
     actions = actions.astype(np.float32).reshape(T, E * P)
     eng = MultiOptEngine(E, 'func4', max_batches=MB, max_history=H)
-    assert eng.many_kernel == 'multi_persist4_kernel<4,5>'
+    assert eng.many_kernel == 'multi_persist5_kernel<4,5>'
     got, st = _multi_rollout(eng, actions, [25, 25, 20])
     eng.close()
     refs = [OptEnvRunner(OracleMulti(P, max_batches=MB, max_history=H)) for _ in range(E)]
@@ -511,7 +511,7 @@ def test_config5_global_size_on_one_engine():
     sample = [0, 1, 4095, 4096, 8190, 8191]
     actions = np.random.RandomState(8192).uniform(1, 3, (T, E * P)).astype(np.float32)
     eng = MultiOptEngine(E, 'func4', max_batches=MB, max_history=H)
-    assert eng.many_kernel == 'multi_persist4_kernel<4,5>'
+    assert eng.many_kernel == 'multi_persist5_kernel<4,5>'
     got, st = _multi_rollout(eng, actions, [20, 20, 8])
     eng.close()
     refs = [OptEnvRunner(OracleMulti(P, max_batches=MB, max_history=H)) for _ in sample]
