@@ -45,6 +45,8 @@ else
            "net:--workload mlp --hidden 256,256 --batch-size 32 --envs 1024 --steps 10 --warmup 2" \
            "nn:--workload nn --steps 40 --warmup 4" "mnist:--workload mnist"; do
     name=${W%%:*}; args=${W#*:}
+    # ONLY: a space-separated subset of the workload names to run
+    if [ -n "${ONLY:-}" ] && ! echo " $ONLY " | grep -q " $name "; then continue; fi
     timeout -k 10 500 python bench.py $args --cpu-seconds 10 --measure-traffic > $OUT/bench_$name.log 2>&1; rc=$?
     echo "bench $name rc=$rc"; summ $OUT/bench_$name.log $name; fatal $rc
     [ "$name" = multi20 ] && continue
@@ -52,6 +54,7 @@ else
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$name -o run --output-format csv -- python3 bench.py $pargs --profile-only --steps 10 --warmup 2 > $OUT/prof_$name.log 2>&1; rc=$?
     echo "rocprof $name rc=$rc"; fatal $rc
   done
+  if [ -n "${ONLY:-}" ]; then echo PART_B_OK; exit 0; fi
   # config 4's global batch on one GPU: the open-loop value and the
   # closed-loop (one launch per step) rate at 32,768 envs
   timeout -k 10 300 python bench.py --envs 32768 --steps 2000 --warmup 200 --no-cpu-baseline --no-measure-traffic > $OUT/bench_e32768.log 2>&1; rc=$?
