@@ -16,7 +16,7 @@ if [ "${TESTS:-multi}" != none ]; then
 fi
 for rep in $(seq 1 ${REPS:-2}); do
   for v in ${FORMS:-four three} ${LIBS:-}; do
-    case $v in four|five|three|one) F=$v; L="";; *) F=${LIB_FORM:-}; L=$v;; esac
+    case $v in four|five|six|three|one) F=$v; L="";; *) F=${LIB_FORM:-}; L=$v;; esac
     CE_MULTI_FORM=$F CE_LIB=$L timeout -k 10 300 python -u bench.py --workload multi --no-cpu-baseline \
         --no-measure-traffic > $OUT/bench_${v}_$rep.json 2>> $OUT/bench.err; rc=$?; fatal $rc
     CE_MULTI_FORM=$F CE_LIB=$L timeout -k 10 300 python -u bench.py --workload multi --steps 20 --warmup 5 \
